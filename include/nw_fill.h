@@ -1,0 +1,141 @@
+/*
+ * nw_fill.h -- C ABI of the MI355X-native Needleman-Wunsch score-table fill.
+ *
+ * This is the drop-in seam for the reference's hot path:
+ *
+ *     void compute_table_scores(computation_t *C);   needleman-wunsch.c:583-626
+ *
+ * called once by the driver at needleman-wunsch.c:662, after the tables were
+ * allocated (score-table.c:60-81, walk-table.c:58-79) and seeded
+ * (computation.c:75-125).  Allocation, seeding and the fill all move to the
+ * GPU behind these entry points; the host keeps the CLI, the reader
+ * (read-sequences.c), the traceback (needleman-wunsch.c:209-331) and the
+ * printer (print-table.c), fed from the outputs below.
+ *
+ * Conventions
+ *   s1 = top string (reference C->top_string), L1 = strlen(s1): columns i.
+ *   s2 = side string (C->side_string),         L2 = strlen(s2): rows j.
+ *   Cells (i, j), 0 <= i <= L1, 0 <= j <= L2; "i-major" linear index
+ *   c = i*(L2+1) + j, the reference's cells[col][row] order
+ *   (score-table.c:71-78).
+ *   m, k, d = match bonus, mismatch penalty, indel penalty (int operands,
+ *   needleman-wunsch.c:783-785).  All arithmetic is int32, as in the
+ *   reference; inputs whose scores could overflow int32 are rejected with
+ *   NW_ERR_RANGE (the reference's behaviour there is undefined).
+ *   Direction code of a cell: bit0 = diag, bit1 = up, bit2 = left, set for
+ *   every candidate equal to the cell's score (needleman-wunsch.c:485-503);
+ *   boundary cells: (0,0) = 0, (i,0) = left, (0,j) = up (computation.c:93-120).
+ *
+ * Errors: every entry point returns 0 (NW_OK) or a negative nw_err code and
+ * never exit()s (the reference's check() -> exit(1), dbg.h:96-100, moves to
+ * the caller).  nw_strerror() gives the message; nw_last_error() the detail
+ * of the most recent failure on the calling thread.
+ *
+ * Threading: calls on one nw_table must not overlap; distinct tables may be
+ * used from distinct threads.  Everything is synchronous unless stated.
+ */
+#ifndef NW_FILL_H
+#define NW_FILL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct nw_stats {
+        int32_t  corner;                 /* H[L1][L2] (computation.c:279-280)     */
+        int32_t  greatest_abs_interior;  /* max |H| over i,j >= 1; 0 if none      */
+                                         /* (needleman-wunsch.c:538-541)          */
+        uint32_t branch_count;           /* interior cells with >= 2 directions,  */
+                                         /* wraps like walk-table.c:108-120       */
+} nw_stats;
+
+enum nw_out {
+        NW_OUT_SCORES = 1u,  /* write the int32 score table                */
+        NW_OUT_DIRS   = 2u,  /* write the packed direction codes           */
+        NW_OUT_STATS  = 4u   /* compute greatest_abs_interior/branch_count */
+};
+
+enum nw_err {
+        NW_OK            = 0,
+        NW_ERR_ARG       = -1,  /* bad argument (NULL, negative length, ...)   */
+        NW_ERR_NODEVICE  = -2,  /* no usable gfx950 device                     */
+        NW_ERR_OOM       = -3,  /* device or host allocation failed            */
+        NW_ERR_HIP       = -4,  /* a HIP runtime call failed                   */
+        NW_ERR_RANGE     = -5,  /* int32 overflow possible for these inputs    */
+        NW_ERR_TIMEOUT   = -6,  /* in-kernel hand-off watchdog fired           */
+        NW_ERR_STATE     = -7   /* call out of order (e.g. no sequences set)   */
+};
+
+const char *nw_strerror(int rc);
+const char *nw_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * One-shot fill into host buffers (the direct compute_table_scores analogue).
+ *
+ * H    : NULL or (L1+1)*(L2+1) int32, i-major (cells[i][j] at i*(L2+1)+j).
+ * dirs : NULL or ceil((L1+1)*(L2+1)/2) bytes; cell c's code is the low nibble
+ *        of dirs[c/2] when c is even, the high nibble when c is odd.
+ * stats: NULL or filled; greatest_abs_interior / branch_count are computed
+ *        only when out_mask has NW_OUT_STATS (else 0).
+ * device: HIP device ordinal (-1: $NW_DEVICE or 0).
+ */
+int nw_fill(const char *s1, int64_t L1, const char *s2, int64_t L2,
+            int32_t m, int32_t k, int32_t d, uint32_t out_mask, int device,
+            int32_t *H, uint8_t *dirs, nw_stats *stats);
+
+/* ---------------------------------------------------------------------------
+ * Device-resident table (the 100k x 100k path: the 45 GB table stays in HBM).
+ *
+ * Device layout (DESIGN.md "Data layout in HBM"):
+ *   scores: column-major, pitch ld = nw_table_score_pitch() int32 elements,
+ *           cell (i, j) at element i*ld + 63 + j (the 63-element front pad
+ *           puts every 64-row stripe on a 256-byte boundary);
+ *   dirs  : 32-bit words, one per (64-row stripe g, 8-column group q, lane l):
+ *           word (g*NQ + q)*64 + l, NQ = ceil(L1/8), holds the codes of cells
+ *           (i = 8q+1+s, j = 64g+1+l), s = 0..7, code s in bits [28-4s, 31-4s].
+ */
+typedef struct nw_table nw_table;
+
+/* Allocate for sequences up to max_L1 x max_L2 with the outputs in out_mask. */
+int nw_table_create(int device, int64_t max_L1, int64_t max_L2,
+                    uint32_t out_mask, nw_table **out);
+void nw_table_destroy(nw_table *t);
+
+/* Upload (H2D) the two sequences; L1 <= max_L1, L2 <= max_L2. */
+int nw_table_set_sequences(nw_table *t, const char *s1, int64_t L1,
+                           const char *s2, int64_t L2);
+
+/* Run the fill on the device-resident sequences.  Synchronous.
+ * out_mask must be a subset of the mask given at creation; when it lacks
+ * NW_OUT_SCORES the fill is score-only (only the last column H[L1][*] is
+ * written).  */
+int nw_table_fill(nw_table *t, int32_t m, int32_t k, int32_t d, uint32_t out_mask);
+
+/* Results of the last fill. */
+int nw_table_stats(nw_table *t, nw_stats *st);
+/* Device time (ms) of the last fill kernel alone, and of the whole fill call
+ * (memsets + seeding + fill), both measured with HIP events on the table's
+ * stream. */
+int nw_table_elapsed_ms(nw_table *t, float *fill_kernel_ms, float *fill_call_ms);
+/* Column-chained FNV-1a-64 of the scores and of the direction codes
+ * (DESIGN.md "Parity hashes"): hH = FNV over the 8-byte LE FNV-1a-64 of each
+ * column's int32 LE scores, i = 0..L1; hD likewise over one code byte per
+ * cell.  Computed on the device. */
+int nw_table_hash(nw_table *t, uint64_t *hH, uint64_t *hD);
+/* Copy columns [i0, i1) of the score table to host, dense ((i1-i0)*(L2+1)). */
+int nw_table_copy_scores(nw_table *t, int64_t i0, int64_t i1, int32_t *dst);
+/* Copy the direction codes of columns [i0, i1) to host, one byte per cell. */
+int nw_table_copy_codes(nw_table *t, int64_t i0, int64_t i1, uint8_t *dst);
+/* Copy the last column H[L1][0..L2] (available in score-only mode too). */
+int nw_table_copy_last_column(nw_table *t, int32_t *dst);
+/* Geometry of the device layout (for zero-copy consumers). */
+int64_t nw_table_score_pitch(const nw_table *t);
+/* Waves per workgroup chosen for the last fill (tuning / reporting). */
+int nw_table_waves(const nw_table *t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NW_FILL_H */

@@ -1,0 +1,256 @@
+"""Python binding (ctypes) of the MI355X Needleman-Wunsch fill, include/nw_fill.h.
+
+This mirrors the reference's hot-path seam -- ``compute_table_scores(C)``
+(needleman-wunsch.c:583-626), called once per alignment by the driver at
+needleman-wunsch.c:662 -- as two entry points:
+
+* :func:`fill` -- one-shot fill into host arrays (scores, direction codes,
+  stats), what the CLI's traceback/printer consume;
+* :class:`Table` -- a device-resident table (the 100k x 100k path: the table
+  stays in HBM; hashes, slices and stats are pulled on demand).
+
+The library is required: importing works without it (so CPU-only tooling can
+inspect the module), but every call raises :class:`NWError` when
+``lib/libnwfill.so`` is missing or no gfx950 GPU is visible.  There is no CPU
+fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libnwfill.so")
+
+NW_OUT_SCORES = 1
+NW_OUT_DIRS = 2
+NW_OUT_STATS = 4
+NW_OUT_ALL = NW_OUT_SCORES | NW_OUT_DIRS | NW_OUT_STATS
+
+NW_OK = 0
+NW_ERR_ARG = -1
+NW_ERR_NODEVICE = -2
+NW_ERR_OOM = -3
+NW_ERR_HIP = -4
+NW_ERR_RANGE = -5
+NW_ERR_TIMEOUT = -6
+NW_ERR_STATE = -7
+
+# Exported symbols of include/nw_fill.h (checked by tests/test_abi.py).
+EXPORTS = (
+    "nw_strerror", "nw_last_error", "nw_fill",
+    "nw_table_create", "nw_table_destroy", "nw_table_set_sequences", "nw_table_fill",
+    "nw_table_stats", "nw_table_elapsed_ms", "nw_table_hash", "nw_table_copy_scores",
+    "nw_table_copy_codes", "nw_table_copy_last_column", "nw_table_score_pitch", "nw_table_waves",
+)
+
+
+class NWError(RuntimeError):
+    def __init__(self, rc: int, msg: str):
+        super().__init__(f"{msg} (rc={rc})")
+        self.rc = rc
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("corner", ctypes.c_int32), ("greatest_abs_interior", ctypes.c_int32),
+                ("branch_count", ctypes.c_uint32)]
+
+
+@dataclass(frozen=True)
+class Stats:
+    corner: int
+    greatest_abs_interior: int
+    branch_count: int
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libnwfill.so (raises NWError if it is absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NWError(NW_ERR_STATE, f"{path} not built (run `make -C needleman-wunsch_amd`)")
+    lib = ctypes.CDLL(path)
+    c_i64, c_i32, c_u32, c_p = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p
+    lib.nw_strerror.restype = ctypes.c_char_p
+    lib.nw_strerror.argtypes = [ctypes.c_int]
+    lib.nw_last_error.restype = ctypes.c_char_p
+    lib.nw_last_error.argtypes = []
+    lib.nw_fill.restype = ctypes.c_int
+    lib.nw_fill.argtypes = [ctypes.c_char_p, c_i64, ctypes.c_char_p, c_i64, c_i32, c_i32, c_i32, c_u32,
+                            ctypes.c_int, c_p, c_p, ctypes.POINTER(_Stats)]
+    lib.nw_table_create.restype = ctypes.c_int
+    lib.nw_table_create.argtypes = [ctypes.c_int, c_i64, c_i64, c_u32, ctypes.POINTER(c_p)]
+    lib.nw_table_destroy.restype = None
+    lib.nw_table_destroy.argtypes = [c_p]
+    lib.nw_table_set_sequences.restype = ctypes.c_int
+    lib.nw_table_set_sequences.argtypes = [c_p, ctypes.c_char_p, c_i64, ctypes.c_char_p, c_i64]
+    lib.nw_table_fill.restype = ctypes.c_int
+    lib.nw_table_fill.argtypes = [c_p, c_i32, c_i32, c_i32, c_u32]
+    lib.nw_table_stats.restype = ctypes.c_int
+    lib.nw_table_stats.argtypes = [c_p, ctypes.POINTER(_Stats)]
+    lib.nw_table_elapsed_ms.restype = ctypes.c_int
+    lib.nw_table_elapsed_ms.argtypes = [c_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    lib.nw_table_hash.restype = ctypes.c_int
+    lib.nw_table_hash.argtypes = [c_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    lib.nw_table_copy_scores.restype = ctypes.c_int
+    lib.nw_table_copy_scores.argtypes = [c_p, c_i64, c_i64, c_p]
+    lib.nw_table_copy_codes.restype = ctypes.c_int
+    lib.nw_table_copy_codes.argtypes = [c_p, c_i64, c_i64, c_p]
+    lib.nw_table_copy_last_column.restype = ctypes.c_int
+    lib.nw_table_copy_last_column.argtypes = [c_p, c_p]
+    lib.nw_table_score_pitch.restype = c_i64
+    lib.nw_table_score_pitch.argtypes = [c_p]
+    lib.nw_table_waves.restype = ctypes.c_int
+    lib.nw_table_waves.argtypes = [c_p]
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != NW_OK:
+        lib = load()
+        detail = lib.nw_last_error().decode(errors="replace")
+        raise NWError(rc, f"{what}: {lib.nw_strerror(rc).decode()}: {detail}")
+
+
+def _bytes(s) -> bytes:
+    return s.encode() if isinstance(s, str) else bytes(s)
+
+
+def fill(s1, s2, m: int, k: int, d: int, *, scores: bool = True, dirs: bool = True,
+         stats: bool = True, device: int = -1):
+    """One-shot fill.  Returns (H, codes, Stats).
+
+    H     : int32 array (L1+1, L2+1), H[i, j] = reference cells[i][j].score, or None
+    codes : uint8 array (L1+1, L2+1) of direction codes (bit0 diag, bit1 up,
+            bit2 left), unpacked from the library's nibble output, or None
+    """
+    lib = load()
+    b1, b2 = _bytes(s1), _bytes(s2)
+    L1, L2 = len(b1), len(b2)
+    ncell = (L1 + 1) * (L2 + 1)
+    H = np.empty((L1 + 1, L2 + 1), dtype=np.int32) if scores else None
+    nib = np.empty((ncell + 1) // 2, dtype=np.uint8) if dirs else None
+    st = _Stats()
+    rc = lib.nw_fill(b1, L1, b2, L2, m, k, d, NW_OUT_STATS if stats else 0, device,
+                     H.ctypes.data if H is not None else None,
+                     nib.ctypes.data if nib is not None else None, ctypes.byref(st))
+    _check(rc, "nw_fill")
+    codes = unpack_nibbles(nib, ncell).reshape(L1 + 1, L2 + 1) if dirs else None
+    return H, codes, Stats(st.corner, st.greatest_abs_interior, st.branch_count)
+
+
+def unpack_nibbles(nib: np.ndarray, ncell: int) -> np.ndarray:
+    """Dense nibble plane (cell c -> nibble c of the byte stream, low first)."""
+    out = np.empty(2 * len(nib), dtype=np.uint8)
+    out[0::2] = nib & 0xF
+    out[1::2] = nib >> 4
+    return out[:ncell]
+
+
+class Table:
+    """Device-resident score table (include/nw_fill.h nw_table_*)."""
+
+    def __init__(self, max_L1: int, max_L2: int, out_mask: int = NW_OUT_ALL, device: int = -1):
+        self._lib = load()
+        self._h = ctypes.c_void_p()
+        _check(self._lib.nw_table_create(device, max_L1, max_L2, out_mask, ctypes.byref(self._h)),
+               "nw_table_create")
+        self.L1 = self.L2 = None
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.nw_table_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_sequences(self, s1, s2) -> None:
+        b1, b2 = _bytes(s1), _bytes(s2)
+        _check(self._lib.nw_table_set_sequences(self._h, b1, len(b1), b2, len(b2)),
+               "nw_table_set_sequences")
+        self.L1, self.L2 = len(b1), len(b2)
+
+    def fill(self, m: int, k: int, d: int, out_mask: int = NW_OUT_SCORES | NW_OUT_DIRS) -> None:
+        _check(self._lib.nw_table_fill(self._h, m, k, d, out_mask), "nw_table_fill")
+
+    def stats(self) -> Stats:
+        st = _Stats()
+        _check(self._lib.nw_table_stats(self._h, ctypes.byref(st)), "nw_table_stats")
+        return Stats(st.corner, st.greatest_abs_interior, st.branch_count)
+
+    def elapsed_ms(self):
+        a, b = ctypes.c_float(), ctypes.c_float()
+        _check(self._lib.nw_table_elapsed_ms(self._h, ctypes.byref(a), ctypes.byref(b)),
+               "nw_table_elapsed_ms")
+        return a.value, b.value
+
+    def hash(self):
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self._lib.nw_table_hash(self._h, ctypes.byref(a), ctypes.byref(b)), "nw_table_hash")
+        return a.value, b.value
+
+    def scores(self, i0: int = 0, i1: int | None = None) -> np.ndarray:
+        i1 = self.L1 + 1 if i1 is None else i1
+        out = np.empty((i1 - i0, self.L2 + 1), dtype=np.int32)
+        _check(self._lib.nw_table_copy_scores(self._h, i0, i1, out.ctypes.data), "nw_table_copy_scores")
+        return out
+
+    def codes(self, i0: int = 0, i1: int | None = None) -> np.ndarray:
+        i1 = self.L1 + 1 if i1 is None else i1
+        out = np.empty((i1 - i0, self.L2 + 1), dtype=np.uint8)
+        _check(self._lib.nw_table_copy_codes(self._h, i0, i1, out.ctypes.data), "nw_table_copy_codes")
+        return out
+
+    def last_column(self) -> np.ndarray:
+        out = np.empty(self.L2 + 1, dtype=np.int32)
+        _check(self._lib.nw_table_copy_last_column(self._h, out.ctypes.data), "nw_table_copy_last_column")
+        return out
+
+    @property
+    def waves(self) -> int:
+        return self._lib.nw_table_waves(self._h)
+
+    @property
+    def score_pitch(self) -> int:
+        return self._lib.nw_table_score_pitch(self._h)
+
+
+# ----------------------------------------------------------------- inputs
+def gen_dna(seed: int, n: int) -> bytes:
+    """splitmix64 i.i.d. DNA: base = "ACGT"[z >> 62]."""
+    if n == 0:
+        return b""
+    with np.errstate(over="ignore"):
+        st = np.uint64(seed) + np.arange(1, n + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        z = st
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return np.frombuffer(b"ACGT", dtype=np.uint8)[(z >> np.uint64(62)).astype(np.intp)].tobytes()
+
+
+def fnv1a64(data, h: int = 0xCBF29CE484222325) -> int:
+    """FNV-1a-64 (host side, for small buffers and the column-chain fold)."""
+    mv = memoryview(bytes(data))
+    for b in mv:
+        h ^= b
+        h = (h * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h

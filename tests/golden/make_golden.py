@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Regenerate the golden fixtures in tests/golden/ from the REFERENCE itself.
+
+Run in the build container (where /root/reference exists) after
+`make -C oracle ref`:
+
+    python tests/golden/make_golden.py            # KATs + CLI goldens (seconds)
+    python tests/golden/make_golden.py --big      # + 100k x 100k colchain (minutes)
+
+Sources:
+  * ref_kats.json   -- oracle/_ref/ref_harness: the compiled reference's own
+                       compute_table_scores() (needleman-wunsch.c:583-626) on
+                       the listed inputs; stats + full-table FNV hashes, and the
+                       full tables for tiny cases.
+  * cli_cases.json  -- oracle/_ref/needleman-wunsch: stdout, stderr and exit
+                       status of the reference CLI (needleman-wunsch.c:698-795)
+                       run as `needleman-wunsch` (argv[0] matters: dbg.c:7-15).
+  * big_colchain.json -- 100k x 100k is beyond the reference (1.36 TB of
+                       tables): produced by the clean-room restatement
+                       oracle/libnworacle.so, which ref_kats.json pins against
+                       the reference up to 10k x 10k (parity is transitive).
+Only inputs and outputs are stored; no reference source travels.
+"""
+import argparse
+import ctypes
+import json
+import os
+import struct
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.abspath(os.path.join(HERE, "..", ".."))
+REF_DIR = os.path.join(ROOT, "oracle", "_ref")
+HARNESS = os.path.join(REF_DIR, "ref_harness")
+REF_CLI = os.path.join(REF_DIR, "needleman-wunsch")
+
+# (kind, A, B, m, k, d): kind "gen" -> splitmix64 DNA of lengths A, B
+# (seeds 1, 2); kind "str" -> literal strings.
+KATS = [
+    ("str", "GCATGCU", "GATTACA", 1, 1, 1),
+    ("str", "GAT", "GTA", 1, 1, 1),
+    ("str", "GT", "GT", 1, 1, 1),
+    ("str", "GT", "GA", 1, 1, 1),
+    ("str", "AAAAAAAAAA", "A", 1, 1, 1),
+    ("str", "A", "A", 2, 1, -1),
+    ("str", "", "ACGT", 1, 1, 1),
+    ("str", "ACGT", "", 1, 1, 1),
+    ("str", "", "", 1, 1, 1),
+    ("str", "hello,world!", "yellow~word?", 3, 2, 1),
+    ("str", "AAAA", "AA", 1, 1, 1),
+    ("gen", 1, 1, 1, 1, 1),
+    ("gen", 1, 50, 1, 1, 1),
+    ("gen", 50, 1, 1, 1, 1),
+    ("gen", 63, 64, 1, 1, 1),
+    ("gen", 64, 64, 1, 1, 1),
+    ("gen", 65, 65, 1, 1, 1),
+    ("gen", 100, 100, 1, 1, 1),
+    ("gen", 127, 129, 0, 0, 0),
+    ("gen", 300, 200, 2, 3, 5),
+    ("gen", 200, 300, -1, -2, -3),
+    ("gen", 1000, 777, 1, 1, 1),
+    ("gen", 777, 1000, 1, 1, 1),
+    ("gen", 1000, 1000, 1, 1, 1),
+    ("gen", 1000, 1000, 2, 3, 5),
+    ("gen", 1000, 1000, 5, -4, 2),
+    ("gen", 1000, 1000, 1, 1, -1),
+    ("gen", 4096, 4096, 1, 1, 1),
+    ("gen", 3000, 5000, 4, 2, 3),
+    ("gen", 10000, 10000, 1, 1, 1),
+    ("gen", 10000, 7000, 2, 3, 5),
+]
+FULL_TABLE_MAX_CELLS = 400
+
+CLI_CASES = [
+    # name, args, stdin
+    ("readme_table_q_s_t", ["-q", "-s", "-t", "1", "1", "1"], "GCATGCU GATTACA\n"),
+    ("readme_q", ["-q", "1", "1", "1"], "GCATGCU GATTACA\n"),
+    ("readme_s_t", ["-s", "-t", "1", "1", "1"], "GCATGCU GATTACA\n"),
+    ("readme_l_s_t_u", ["-l", "-s", "-t", "-u", "1", "1", "1"], "GCATGCU GATTACA\n"),
+    ("readme_all_color", ["-c", "-l", "-s", "-t", "1", "1", "1"], "GCATGCU GATTACA\n"),
+    ("readme_color_u", ["-c", "-u", "-t", "-q", "1", "1", "1"], "GCATGCU GATTACA\n"),
+    ("gt_gt", ["1", "1", "1"], "GT GT\n"),
+    ("gt_ga", ["1", "1", "1"], "GT GA\n"),
+    ("gat_gta", ["1", "1", "1"], "GAT GTA\n"),
+    ("gat_gta_s", ["-s", "1", "1", "1"], "GAT GTA\n"),
+    ("gat_gta_l", ["-l", "1", "1", "1"], "GAT GTA\n"),
+    ("gat_gta_lq", ["-l", "-q", "1", "1", "1"], "GAT GTA\n"),
+    ("gat_gta_t", ["-t", "1", "1", "1"], "GAT GTA\n"),
+    ("gat_gta_c", ["-c", "1", "1", "1"], "GAT GTA\n"),
+    ("width_quirk", ["-q", "-t", "1", "1", "1"], "AAAAAAAAAA A\n"),
+    ("negative_operands", ["-s", "-t", "--", "2", "1", "-1"], "GATTA GCAT\n"),
+    ("zero_operands", ["-s", "-l", "0", "0", "0"], "ACG TG\n"),
+    ("many_alignments", ["-s", "-l", "1", "1", "1"], "AAAA AA\n"),
+    ("empty_s1", ["-s", "-t", "1", "1", "1"], "   ACGT\n"),
+    ("empty_s1_s2", ["-s", "-t", "1", "1", "1"], "\n\n  \n"),
+    ("third_token_ignored", ["-s", "-l", "1", "1", "1"], "ACGT AGT CCCC\n"),
+    ("multiline", ["-s", "1", "1", "1"], "ACGTTGCA\n\n\tAGTTCA"),
+    ("threads_p2", ["-p", "2", "-s", "-t", "1", "1", "1"], "GCATGCU GATTACA\n"),
+    ("random_20", ["-s", "-l", "-t", "-u", "1", "1", "1"], "GGTCCTTGCTCGAACGTGCA GGGTCCGGCGCCTATTCAGA\n"),
+    ("random_quiet_summary", ["-q", "-s", "2", "3", "5"],
+     "GGTCCTTGCTCGAACGTGCAGATACAGTTAGCCA GGGTCCGGCGCCTATTCAGACGGAACCTGTTA\n"),
+    ("file_input", ["-s", "-f", "{FILE}", "1", "1", "1"], "GATTACA GCATGCU\n"),
+    # error paths (all exit 1)
+    ("err_no_operands", [], "A B\n"),
+    ("err_two_operands", ["1", "1"], "A B\n"),
+    ("err_four_operands", ["1", "1", "1", "1"], "A B\n"),
+    ("err_p1", ["-p", "1", "1", "1", "1"], "A B\n"),
+    ("err_help", ["-h"], ""),
+    ("err_bad_option", ["-x", "1", "1", "1"], "A B\n"),
+    ("err_missing_p_arg", ["-p"], ""),
+    ("err_eof_one_token", ["1", "1", "1"], "ACGT"),
+    ("err_eof_empty", ["1", "1", "1"], ""),
+    ("err_no_file", ["-f", "/nonexistent/nw_input.txt", "1", "1", "1"], ""),
+]
+
+
+def run_harness(kind, a, b, m, k, d, dump=None):
+    args = [HARNESS, kind, str(a), str(b), str(m), str(k), str(d), "1"]
+    if dump:
+        args.append(dump)
+    return json.loads(subprocess.check_output(args))
+
+
+def make_kats():
+    out = []
+    for kind, a, b, m, k, d in KATS:
+        with tempfile.NamedTemporaryFile(suffix=".bin") as tf:
+            r = run_harness(kind, a, b, m, k, d, tf.name)
+            case = {"kind": kind, "m": m, "k": k, "d": d, "L1": r["L1"], "L2": r["L2"],
+                    "corner": r["corner"], "gav": r["gav"], "branch_count": r["branch_count"],
+                    "hH": r["hH"], "hD": r["hD"]}
+            if kind == "str":
+                case["s1"], case["s2"] = a, b
+            ncell = (r["L1"] + 1) * (r["L2"] + 1)
+            if ncell <= FULL_TABLE_MAX_CELLS:
+                raw = open(tf.name, "rb").read()
+                case["H"] = list(struct.unpack("<%di" % ncell, raw[:4 * ncell]))
+                case["codes"] = list(raw[4 * ncell:5 * ncell])
+        out.append(case)
+        print("kat", kind, case["L1"], case["L2"], m, k, d, case["corner"], case["hH"], file=sys.stderr)
+    return out
+
+
+def run_cli(binary, args, stdin, file_content=None):
+    tmp = None
+    if any("{FILE}" in a for a in args):
+        tmp = tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False)
+        tmp.write(file_content if file_content is not None else stdin)
+        tmp.close()
+        args = [tmp.name if a == "{FILE}" else a for a in args]
+        stdin = ""
+    try:
+        p = subprocess.run(["needleman-wunsch"] + args, executable=binary, input=stdin.encode(),
+                           capture_output=True, timeout=120)
+    finally:
+        if tmp:
+            os.unlink(tmp.name)
+    return p.returncode, p.stdout, p.stderr
+
+
+def make_cli():
+    out = []
+    for name, args, stdin in CLI_CASES:
+        rc, so, se = run_cli(REF_CLI, args, stdin)
+        out.append({"name": name, "args": args, "stdin": stdin, "rc": rc,
+                    "stdout": so.decode("utf-8"), "stderr": se.decode("utf-8")})
+        print("cli", name, rc, len(so), len(se), file=sys.stderr)
+    return out
+
+
+def make_big():
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "libnworacle.so"))
+
+    class St(ctypes.Structure):
+        _fields_ = [("corner", ctypes.c_int32), ("gav", ctypes.c_int32), ("bc", ctypes.c_uint32)]
+
+    out = []
+    for L1, L2, m, k, d in [(100000, 100000, 1, 1, 1)]:
+        b1, b2 = ctypes.create_string_buffer(L1), ctypes.create_string_buffer(L2)
+        lib.nwo_gen_dna(ctypes.c_uint64(1), ctypes.c_int64(L1), b1)
+        lib.nwo_gen_dna(ctypes.c_uint64(2), ctypes.c_int64(L2), b2)
+        st, h1, h2 = St(), ctypes.c_uint64(), ctypes.c_uint64()
+        lib.nwo_fill_colchain(b1, ctypes.c_int64(L1), b2, ctypes.c_int64(L2), m, k, d,
+                              ctypes.byref(h1), ctypes.byref(h2), ctypes.byref(st))
+        out.append({"L1": L1, "L2": L2, "m": m, "k": k, "d": d, "corner": st.corner, "gav": st.gav,
+                    "branch_count": st.bc, "hH2": "%016x" % h1.value, "hD2": "%016x" % h2.value,
+                    "source": "oracle/libnworacle.so nwo_fill_colchain (restatement; transitive parity)"})
+        print("big", out[-1], file=sys.stderr)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--big", action="store_true")
+    a = ap.parse_args()
+    if not os.path.exists(HARNESS):
+        sys.exit("build the reference first: make -C oracle ref")
+    with open(os.path.join(HERE, "ref_kats.json"), "w") as f:
+        json.dump(make_kats(), f, indent=0)
+    with open(os.path.join(HERE, "cli_cases.json"), "w") as f:
+        json.dump(make_cli(), f, indent=1, ensure_ascii=False)
+    if a.big:
+        with open(os.path.join(HERE, "big_colchain.json"), "w") as f:
+            json.dump(make_big(), f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

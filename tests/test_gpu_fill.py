@@ -1,0 +1,158 @@
+"""GPU parity: the HIP fill (through the C ABI) against the reference goldens
+and the CPU oracle.  Bit-exact on every cell (integer work).
+
+Runs on an MI355X only (`pytest -m gpu`).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import nw_amd
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+ALL = nw_amd.NW_OUT_ALL
+
+
+@pytest.fixture
+def waves(monkeypatch):
+    """Force the workgroup height (waves per WG) the library picks."""
+    def _set(w):
+        if w is None:
+            monkeypatch.delenv("NW_WAVES", raising=False)
+        else:
+            monkeypatch.setenv("NW_WAVES", str(w))
+    yield _set
+    monkeypatch.delenv("NW_WAVES", raising=False)
+
+
+def _check_against_oracle(s1, s2, m, k, d):
+    H, D, st = nw_amd.fill(s1, s2, m, k, d)
+    Ho, Do, sto = O.fill(s1, s2, m, k, d)
+    assert H.shape == Ho.shape
+    if not np.array_equal(H, Ho):
+        bad = np.argwhere(H != Ho)
+        raise AssertionError(f"score mismatch at {len(bad)} cells, first {bad[:5].tolist()} "
+                             f"got {H[tuple(bad[0])]} want {Ho[tuple(bad[0])]}")
+    if not np.array_equal(D, Do):
+        bad = np.argwhere(D != Do)
+        raise AssertionError(f"code mismatch at {len(bad)} cells, first {bad[:5].tolist()}")
+    assert (st.corner, st.greatest_abs_interior, st.branch_count) == sto
+
+
+def test_reference_kats(ref_kats):
+    """Every KAT of the compiled reference: stats + full-table hashes."""
+    for case in ref_kats:
+        s1, s2 = O.kat_inputs(case)
+        H, D, st = nw_amd.fill(s1, s2, case["m"], case["k"], case["d"])
+        assert (st.corner, st.greatest_abs_interior, st.branch_count) == \
+            (case["corner"], case["gav"], case["branch_count"]), case
+        assert "%016x" % O.fnv(H) == case["hH"], case
+        assert "%016x" % O.fnv(D) == case["hD"], case
+        if "H" in case:
+            assert H.ravel().tolist() == case["H"]
+            assert D.ravel().tolist() == case["codes"]
+
+
+@pytest.mark.parametrize("L1,L2", [(1, 1), (1, 64), (64, 1), (8, 63), (9, 65), (17, 128), (16, 129),
+                                   (255, 257), (513, 1025), (1000, 3000), (3000, 1000)])
+def test_shapes_vs_oracle(L1, L2):
+    _check_against_oracle(O.gen_dna(11, L1), O.gen_dna(12, L2), 1, 1, 1)
+
+
+@pytest.mark.parametrize("m,k,d", [(1, 1, 1), (2, 3, 5), (5, -4, 2), (1, 1, -1), (0, 0, 0),
+                                   (-3, 2, 1), (7, 7, 0), (100, 1000, 37), (1, 1, 20000)])
+def test_params_vs_oracle(m, k, d):
+    _check_against_oracle(O.gen_dna(3, 700), O.gen_dna(4, 900), m, k, d)
+
+
+@pytest.mark.parametrize("w", [1, 2, 4, 6, 8, 16])
+def test_every_workgroup_height(waves, w):
+    """Each WG height; L2 spans many WG-stripes so the granule hand-off runs."""
+    waves(w)
+    _check_against_oracle(O.gen_dna(5, 1234), O.gen_dna(6, 64 * w * 5 + 17), 2, 3, 5)
+
+
+def test_many_workgroup_stripes_handoff(waves):
+    """W=1: 157 WG-stripes, every boundary through the granule hand-off."""
+    waves(1)
+    _check_against_oracle(O.gen_dna(7, 2000), O.gen_dna(8, 10000), 1, 1, 1)
+
+
+def test_arbitrary_bytes_and_ties():
+    rng = np.random.default_rng(0)
+    s1 = bytes(rng.integers(1, 256, 1500, dtype=np.uint8))
+    s2 = bytes(rng.integers(1, 256, 1300, dtype=np.uint8))
+    _check_against_oracle(s1, s2, 3, 2, 1)
+    _check_against_oracle(b"A" * 900, b"A" * 700, 1, 1, 1)        # all matches
+    _check_against_oracle(b"A" * 900, b"C" * 700, 0, 0, 0)        # every cell ties 3 ways
+    _check_against_oracle(b"ACGT" * 300, b"TGCA" * 200, 1, 2, 1)
+
+
+@pytest.mark.parametrize("s1,s2", [(b"", b""), (b"", b"ACGT"), (b"ACGT", b""), (b"A", b"")])
+def test_empty_sequences(s1, s2):
+    _check_against_oracle(s1, s2, 1, 1, 1)
+
+
+def test_overflow_is_rejected():
+    with pytest.raises(nw_amd.NWError) as e:
+        nw_amd.fill(b"ACGT" * 1000, b"ACGT" * 1000, 1, 1, 1 << 20)
+    assert e.value.rc == nw_amd.NW_ERR_RANGE
+
+
+def test_table_api_slices_hash_and_score_only():
+    s1, s2 = O.gen_dna(21, 3001), O.gen_dna(22, 2003)
+    Ho, Do, sto = O.fill(s1, s2, 2, 3, 5)
+    with nw_amd.Table(4000, 4000) as t:
+        t.set_sequences(s1, s2)
+        t.fill(2, 3, 5, ALL)
+        st = t.stats()
+        assert (st.corner, st.greatest_abs_interior, st.branch_count) == sto
+        assert np.array_equal(t.scores(100, 357), Ho[100:357])
+        assert np.array_equal(t.codes(2990, 3002), Do[2990:3002])
+        assert np.array_equal(t.last_column(), Ho[-1])
+        h, e, _ = O.colchain(s1, s2, 2, 3, 5)
+        assert t.hash() == (h, e)
+        kms, cms = t.elapsed_ms()
+        assert 0 < kms <= cms
+        # refill is idempotent
+        t.fill(2, 3, 5, ALL)
+        assert t.hash() == (h, e)
+        # score-only: corner and last column without the table
+        t.fill(2, 3, 5, nw_amd.NW_OUT_STATS)
+        st2 = t.stats()
+        assert (st2.corner, st2.greatest_abs_interior, st2.branch_count) == sto
+        assert np.array_equal(t.last_column(), Ho[-1])
+        # dirs-only
+        t.fill(2, 3, 5, nw_amd.NW_OUT_DIRS)
+        assert np.array_equal(t.codes(0, 40), Do[0:40])
+
+
+def test_score_only_table_without_score_storage():
+    s1, s2 = O.gen_dna(31, 5000), O.gen_dna(32, 4000)
+    c, hl = O.score_only(s1, s2, 1, 1, 1)
+    with nw_amd.Table(5000, 4000, nw_amd.NW_OUT_STATS) as t:
+        t.set_sequences(s1, s2)
+        t.fill(1, 1, 1, 0)
+        assert t.stats().corner == c
+        assert O.fnv(t.last_column()) == hl
+        with pytest.raises(nw_amd.NWError):
+            t.fill(1, 1, 1, nw_amd.NW_OUT_SCORES)
+
+
+def test_10k_config_c2(ref_kats):
+    """configs[1]: 10k x 10k random DNA, 1 1 1 -- full tables vs the reference."""
+    case = next(c for c in ref_kats if c["kind"] == "gen" and c["L1"] == 10000 and c["L2"] == 10000)
+    s1, s2 = O.kat_inputs(case)
+    with nw_amd.Table(10000, 10000) as t:
+        t.set_sequences(s1, s2)
+        t.fill(1, 1, 1, ALL)
+        st = t.stats()
+        assert (st.corner, st.greatest_abs_interior, st.branch_count) == \
+            (case["corner"], case["gav"], case["branch_count"])
+        H = t.scores()
+        D = t.codes()
+    assert "%016x" % O.fnv(H) == case["hH"]
+    assert "%016x" % O.fnv(D) == case["hD"]
