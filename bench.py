@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--L2", type=int, default=100_000)
     ap.add_argument("--mkd", type=int, nargs=3, default=(1, 1, 1))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--outputs", default="sd",
+                    help="what the fill writes: s = scores, d = direction codes, t = stats "
+                         "('' = score-only); the metric's workload is 'sd'")
     ap.add_argument("--cpu-sample", type=int, default=14142,
                     help="side of the square sample the CPU reference fills (~2e8 cells)")
     return ap.parse_args()
@@ -92,8 +95,9 @@ def run_single(a):
     m, k, d = a.mkd
     L1, L2 = a.L1, a.L2
     s1, s2 = nw_amd.gen_dna(1, L1), nw_amd.gen_dna(2, L2)
-    mask = nw_amd.NW_OUT_SCORES | nw_amd.NW_OUT_DIRS
-    t = nw_amd.Table(L1, L2, mask)
+    mask = ((nw_amd.NW_OUT_SCORES if "s" in a.outputs else 0) | (nw_amd.NW_OUT_DIRS if "d" in a.outputs else 0)
+            | (nw_amd.NW_OUT_STATS if "t" in a.outputs else 0))
+    t = nw_amd.Table(L1, L2, mask | nw_amd.NW_OUT_STATS)
     t.set_sequences(s1, s2)
     for _ in range(a.warmup):
         t.fill(m, k, d, mask)
@@ -120,7 +124,8 @@ def main():
     cells = L1 * L2
     value = cells / (ms * 1e-3) / 1e9
     kern_ms = sum(kern) / len(kern)
-    alg_bytes = BYTES_PER_CELL * (L1 + 1) * (L2 + 1)
+    bpc = (4.0 if "s" in a.outputs else 0.0) + (0.5 if "d" in a.outputs else 0.0)
+    alg_bytes = bpc * (L1 + 1) * (L2 + 1)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     tr = latest_traffic(L1, L2)
     out = {
@@ -128,12 +133,13 @@ def main():
         "value": round(value, 2), "unit": "GCUPS", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "int32", "data": "synthetic (splitmix64 DNA, seeds 1/2)",
-        "config": {"workload": f"{L1}x{L2} full-table fill (scores+direction codes), "
-                               f"m,k,d={a.mkd[0]},{a.mkd[1]},{a.mkd[2]}",
+        "config": {"workload": f"{L1}x{L2} " + ("full-table fill (scores+direction codes)" if a.outputs == "sd"
+                                                 else f"fill writing '{a.outputs}'") +
+                               f", m,k,d={a.mkd[0]},{a.mkd[1]},{a.mkd[2]}",
                    "L1": L1, "L2": L2, "parallelism": "single GPU", "waves_per_wg": waves,
                    "corner": corner},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "bytes_per_cell": bpc,
                      "traffic": tr["hbm_bytes_per_launch"] if tr else None,
                      "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes,
                      "kernel_gcups": round(cells / (kern_ms * 1e-3) / 1e9, 2)},

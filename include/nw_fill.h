@@ -89,9 +89,11 @@ int nw_fill(const char *s1, int64_t L1, const char *s2, int64_t L2,
  * Device-resident table (the 100k x 100k path: the 45 GB table stays in HBM).
  *
  * Device layout (DESIGN.md "Data layout in HBM"):
- *   scores: column-major, pitch ld = nw_table_score_pitch() int32 elements,
- *           cell (i, j) at element i*ld + 63 + j (the 63-element front pad
- *           puts every 64-row stripe on a 256-byte boundary);
+ *   scores: stripe-major tiles.  Rows j >= 1 are grouped in 64-row stripes
+ *           g = (j-1)/64, lane l = (j-1)%64; cell (i, j) is element
+ *           g*P + i*64 + l with P = nw_table_score_pitch() = (L1+1)*64, so one
+ *           column of one stripe is 256 contiguous bytes and a stripe's columns
+ *           follow each other.  Row 0 (H[i][0] = -i*d) is kept apart.
  *   dirs  : 32-bit words, one per (64-row stripe g, 8-column group q, lane l):
  *           word (g*NQ + q)*64 + l, NQ = ceil(L1/8), holds the codes of cells
  *           (i = 8q+1+s, j = 64g+1+l), s = 0..7, code s in bits [28-4s, 31-4s].

@@ -41,7 +41,6 @@
 namespace {
 
 constexpr int CH = 8;                 // columns per chunk (= codes per dirs word)
-constexpr int PADROWS = 63;           // front pad of each score column
 constexpr int64_t SPIN_TICKS = 200000000;  // 2 s of s_memrealtime (100 MHz)
 
 enum CtlWord { CTL_NEXT = 0, CTL_ABORT = 1, CTL_GAV = 2, CTL_BC = 3, CTL_ERR = 4, CTL_WORDS = 16 };
@@ -54,8 +53,8 @@ struct FillArgs {
     int32_t NC;             // chunks = ceil(L1 / 8)
     int32_t NG;             // wave stripes = ceil(L2 / 64)
     int32_t NSW;            // workgroup stripes = ceil(NG / W)
-    int32_t* H;             // scores: (i, j) at H[i*ldh + 63 + j]
-    int64_t ldh;
+    int32_t* H;             // score tiles: (i, j>=1) at H[(g*(L1+1) + i)*64 + l], j-1 = 64g+l
+    int64_t spitch;         // (L1+1)*64: elements per stripe
     uint32_t* D;            // codes: word ((g*NC + q)*64 + lane)
     int32_t* lastcol;       // score-only: H[L1][j] at lastcol[63 + j]
     uint64_t* gran;         // boundary granules, slot s at gran + s*gpitch
@@ -84,6 +83,8 @@ __device__ __forceinline__ int wave_prefix_max(int y) {
     return y;
 }
 
+typedef const __attribute__((address_space(4))) uint64_t* cptr64;
+
 __device__ __forceinline__ int iabs(int v) { return v < 0 ? -v : v; }
 
 // Count nibbles of a codes word that have >= 2 of their 3 direction bits.
@@ -91,6 +92,11 @@ __device__ __forceinline__ uint32_t branch_nibbles(uint32_t x) {
     uint32_t y = (x & (x >> 1)) | (x & (x >> 2)) | ((x >> 1) & (x >> 2));
     return __builtin_popcount(y & 0x11111111u);
 }
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
+// (lgkmcnt) and syncs.  Unlike __syncthreads() it carries no fence, so it
+// never waits for the wave's in-flight global stores (vmcnt).
+__device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Wave-uniform copies of per-wave values (so address math stays scalar).
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -109,17 +115,23 @@ struct WaveState {
 // Cell recurrence = needleman-wunsch.c:429-465; direction flags :485-503.
 template <bool SH, bool SD, bool ST, bool LAST>
 __device__ __forceinline__ void chunk_body(const FillArgs& a, WaveState& st, const int* T,
-                                           int c, int nstep, int lane, int64_t hcol_off,
-                                           int d, int cm, int ck, int* bot_lds, uint32_t* dword_out) {
-    // s1[8c .. 8c+7]: one uniform 8-byte (scalar) load.
-    const uint64_t ch8 = *reinterpret_cast<const uint64_t*>(a.s1 + 8 * (int64_t)c);
+                                           int c, int nstep, int lane, int64_t tile_off, int j0,
+                                           int d, int vcm, int vck, int* bot_wr, uint32_t* dword_out) {
+    // s1[8c .. 8c+7]: one uniform 8-byte load through the constant address
+    // space -> s_load_dwordx2 (lgkmcnt), never a vector load that would make
+    // the wave wait for its own in-flight score stores.
+    const uint64_t ch8 = *(cptr64)(a.s1 + 8 * (int64_t)c);
     uint32_t acc = 0;
-    int32_t* hbase = a.H + hcol_off + (int64_t)(8 * c + 1) * a.ldh;
+    // Buffer descriptor on this chunk's 8 column segments (2 KB contiguous in
+    // the stripe-major tile layout): per-step addresses are lane*4 (VGPR) +
+    // s*256 (SGPR) -- no VALU address math.
+    int32_t* cb = a.H + tile_off + (int64_t)(8 * c + 1) * 64;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(cb, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
         if (LAST && s >= nstep) break;
         const uint32_t ch = (uint32_t)(ch8 >> (8 * s)) & 0xffu;
-        const int sub = (ch == st.c2) ? cm : ck;          // m+d or d-k
+        const int sub = (ch == st.c2) ? vcm : vck;        // m+d or d-k
         const int sh = wave_shr1(st.Tprev, st.G);         // G[l-1], lane 0: row above
         const int dg = sh + sub;                          // diag candidate (shifted)
         const int lf = st.G - d;                          // left candidate (shifted)
@@ -127,36 +139,45 @@ __device__ __forceinline__ void chunk_body(const FillArgs& a, WaveState& st, con
         const int Y = max(max(lf, dg), top);
         const int G = wave_prefix_max(Y);                 // resolves all "up" terms
         const int Hv = G - st.laneoff;
-        if (SH) hbase[(int64_t)s * a.ldh + lane] = Hv;
+        if (SH) __builtin_amdgcn_raw_buffer_store_b32(Hv, rs, lane * 4, s * 256, 0);
         if (SD || ST) {                                   // codes also feed branch_count
             const int up = wave_shr1(top, G);             // up candidate (shifted)
             acc = (acc << 4) | (uint32_t)(G == dg) | ((uint32_t)(G == up) << 1) |
                   ((uint32_t)(G == lf) << 2);
         }
         if (ST) st.gav = max(st.gav, iabs(Hv));
-        if (lane == 63) bot_lds[s] = G;
+        bot_wr[s] = G;   // lane 63 -> bottom-row slot, lanes 0..62 -> scratch
         st.G = G;
         st.Tprev = top;
         if (LAST && !SH && s == nstep - 1) {
             // score-only: keep the last column H[L1][*].
-            a.lastcol[hcol_off + lane] = Hv;
+            a.lastcol[j0 + lane] = Hv;
         }
     }
     if (LAST && nstep < CH) acc <<= 4 * (CH - nstep);
     *dword_out = acc;
 }
 
+// Workgroup = W compute waves (64-row stripes, stacked) + 1 loader wave.
+// The loader feeds the top row of the WG-stripe for chunk t+1 into LDS while
+// the compute waves run superstep t; it issues no stores, so its waits on
+// the hand-off loads are exact, and the compute waves never wait on vmcnt.
 template <int W, bool SH, bool SD, bool ST>
-__global__ __launch_bounds__(64 * W) void nw_fill_kernel(FillArgs a) {
-    __shared__ __attribute__((aligned(16))) int xfer[(W + 1) * 2 * CH];
+__global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
+    // xfer[w][par][8]: top row of wave w (w = 0: from the loader, else the
+    // bottom row of wave w-1) for chunk parity par.  Then 72 scratch dwords.
+    constexpr int XFER = (W + 1) * 2 * CH;
+    __shared__ __attribute__((aligned(16))) int xfer[XFER + 64 + CH];
     __shared__ int sh_sidx;
     __shared__ int sh_abort;
 
     const int lane = threadIdx.x & 63;
     const int w = uni(threadIdx.x >> 6);
+    const bool loader = (w == W);
     const int d = a.d;
-    const int cm = a.m + a.d;
-    const int ck = a.d - a.k;
+    int vcm = a.m + a.d;
+    int vck = a.d - a.k;
+    asm volatile("" : "+v"(vcm), "+v"(vck));   // keep both as VGPR operands of v_cndmask
     const int NC = a.NC;
     const int nlast = a.L1 - CH * (NC - 1);   // steps in the last chunk (1..8)
 
@@ -169,94 +190,112 @@ __global__ __launch_bounds__(64 * W) void nw_fill_kernel(FillArgs a) {
         const int sidx = uni(sh_sidx);
         if (sidx >= a.NSW || sh_abort) break;
 
-        const int g = sidx * W + w;                // wave stripe
-        const bool real = g < a.NG;
+        const int g = sidx * W + w;                // wave stripe (compute waves)
+        const bool real = !loader && g < a.NG;
         const int j0 = 1 + 64 * g;                 // first row of the wave stripe
         const int jrow = j0 + lane;
+        const int64_t tile_off = (int64_t)g * a.spitch;
         WaveState st;
-        st.c2 = a.s2[jrow - 1];
+        st.c2 = real ? a.s2[jrow - 1] : 0u;
         st.laneoff = (64 * w + lane) * d;
         // column 0: H[0][j] = -j*d  ->  G = -(1 + 64*sidx*W)*d for every lane.
         st.G = -(1 + 64 * sidx * W) * d;
         st.Tprev = st.G;
         st.gav = 0;
         st.bc = 0;
-        const int64_t hcol_off = PADROWS + (int64_t)j0;
 
-        // wave 0: prefetch register for the boundary granules of chunk 0.
+        // ---- loader state: top row of this WG-stripe, one chunk ahead ----
         const uint64_t* gin = a.gran + (int64_t)(sidx % a.nslot) * a.gpitch;
         uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
         uint64_t pf = 0;
-        if (w == 0 && sidx > 0 && lane < CH)
-            pf = __hip_atomic_load(gin + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-
-        const int nsuper = NC + W - 1;
-        for (int t = 0; t < nsuper; ++t) {
-            const int c = t - w;
-            if (real && c >= 0 && c < NC) {
-                const int par = c & 1;
-                int* top_lds = &xfer[(w * 2 + par) * CH];
-                int* bot_lds = &xfer[((w + 1) * 2 + par) * CH];
-                const int nstep = (c == NC - 1) ? nlast : CH;
-                if (w == 0) {
-                    // Top row of the WG-stripe for columns 8c+1 .. 8c+8.
-                    if (sidx == 0) {
-                        // row 0: H[i][0] - d = -(i+1)*d   (computation.c:102-110)
-                        if (lane < CH) top_lds[lane] = -(CH * c + 2 + lane) * d;
-                    } else {
-                        const uint32_t want = (uint32_t)sidx;
-                        bool ok = lane >= nstep || (uint32_t)(pf >> 32) == want;
-                        if (!__all(ok)) {
-                            const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-                            for (;;) {
-                                __builtin_amdgcn_s_sleep(1);
-                                if (!ok)
-                                    pf = __hip_atomic_load(gin + CH * (int64_t)c + lane, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-                                ok = lane >= nstep || (uint32_t)(pf >> 32) == want;
-                                if (__all(ok)) break;
-                                const int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
-                                const uint32_t ab = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT);
-                                if (ab || now - t0 > SPIN_TICKS) {
-                                    if (lane == 0) {
-                                        __hip_atomic_store(&a.ctl[CTL_ABORT], 1u, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-                                        if (!ab) atomicCAS(&a.ctl[CTL_ERR], 0u, (uint32_t)NW_ERR_TIMEOUT);
-                                        sh_abort = 1;
-                                    }
-                                    break;
-                                }
-                            }
+        // Fill xfer[0][par(c)] with chunk c's top values (G domain of row "-1").
+        auto loader_fill = [&](int c) {
+            int* dst = &xfer[(c & 1) * CH];
+            const int n = (c == NC - 1) ? nlast : CH;
+            if (sidx == 0) {
+                // row 0: H[i][0] - d = -(i+1)*d   (computation.c:102-110)
+                if (lane < CH) dst[lane] = -(CH * c + 2 + lane) * d;
+                return;
+            }
+            const uint32_t want = (uint32_t)sidx;
+            bool ok = lane >= n || (uint32_t)(pf >> 32) == want;
+            if (!__all(ok)) {
+                const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (!ok)
+                        pf = __hip_atomic_load(gin + CH * (int64_t)c + lane, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                    ok = lane >= n || (uint32_t)(pf >> 32) == want;
+                    if (__all(ok)) break;
+                    const int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
+                    const uint32_t ab = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                    if (ab || now - t0 > SPIN_TICKS) {
+                        if (lane == 0) {
+                            __hip_atomic_store(&a.ctl[CTL_ABORT], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (!ab) atomicCAS(&a.ctl[CTL_ERR], 0u, (uint32_t)NW_ERR_TIMEOUT);
+                            sh_abort = 1;
                         }
-                        if (lane < CH) top_lds[lane] = (int)(uint32_t)pf;
-                        if (c + 1 < NC && lane < CH)
-                            pf = __hip_atomic_load(gin + CH * (int64_t)(c + 1) + lane, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
+                        break;
                     }
                 }
-                const int4 t03 = *reinterpret_cast<const int4*>(top_lds);
-                const int4 t47 = *reinterpret_cast<const int4*>(top_lds + 4);
-                const int T[CH] = {t03.x, t03.y, t03.z, t03.w, t47.x, t47.y, t47.z, t47.w};
-                uint32_t dw;
-                if (c == NC - 1)
-                    chunk_body<SH, SD, ST, true>(a, st, T, c, nstep, lane, hcol_off, d, cm, ck, bot_lds, &dw);
-                else
-                    chunk_body<SH, SD, ST, false>(a, st, T, c, CH, lane, hcol_off, d, cm, ck, bot_lds, &dw);
-                const bool rowok = jrow <= a.L2;
-                if (!rowok) dw = 0;
-                if (SD) a.D[((int64_t)g * NC + c) * 64 + lane] = dw;
-                if (ST) st.bc += branch_nibbles(dw);
-                // Last wave of a non-final WG-stripe publishes its bottom row.
-                if (w == W - 1 && sidx + 1 < a.NSW && lane < nstep) {
-                    const int v = bot_lds[lane] - 64 * W * d;     // -> "row above" domain
-                    const uint64_t gr = ((uint64_t)(uint32_t)(sidx + 1) << 32) | (uint32_t)v;
-                    __hip_atomic_store(gout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
+            }
+            if (lane < CH) dst[lane] = (int)(uint32_t)pf;
+            if (c + 1 < NC && lane < CH)          // prefetch the next chunk
+                pf = __hip_atomic_load(gin + CH * (int64_t)(c + 1) + lane, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+        };
+        if (loader) {
+            // ---------------- loader wave: no stores, exact waits ----------------
+            if (sidx > 0 && lane < CH)
+                pf = __hip_atomic_load(gin + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            loader_fill(0);
+            wg_barrier();
+            if (!sh_abort) {
+                const int nsuper = NC + W - 1;
+                for (int t = 0; t < nsuper; ++t) {
+                    if (t + 1 < NC) loader_fill(t + 1);
+                    wg_barrier();
+                    if (sh_abort) break;
                 }
             }
-            __syncthreads();
-            if (sh_abort) break;
+        } else {
+            // ---------------- compute waves: one chunk per superstep ------------
+            wg_barrier();
+            if (!sh_abort) {
+                const int nsuper = NC + W - 1;
+                for (int t = 0; t < nsuper; ++t) {
+                    const int c = t - w;
+                    if (real && c >= 0 && c < NC) {
+                        const int par = c & 1;
+                        const int* top_lds = &xfer[(w * 2 + par) * CH];
+                        // Bottom row goes to xfer[w+1][par]; lanes 0..62 hit scratch.
+                        int* bot_wr = (lane == 63) ? &xfer[((w + 1) * 2 + par) * CH] : &xfer[XFER + lane];
+                        const int nstep = (c == NC - 1) ? nlast : CH;
+                        const int4 t03 = *reinterpret_cast<const int4*>(top_lds);
+                        const int4 t47 = *reinterpret_cast<const int4*>(top_lds + 4);
+                        const int T[CH] = {t03.x, t03.y, t03.z, t03.w, t47.x, t47.y, t47.z, t47.w};
+                        uint32_t dw;
+                        if (c == NC - 1)
+                            chunk_body<SH, SD, ST, true>(a, st, T, c, nstep, lane, tile_off, j0, d, vcm, vck, bot_wr, &dw);
+                        else
+                            chunk_body<SH, SD, ST, false>(a, st, T, c, CH, lane, tile_off, j0, d, vcm, vck, bot_wr, &dw);
+                        if (jrow > a.L2) dw = 0;
+                        if (SD) a.D[((int64_t)g * NC + c) * 64 + lane] = dw;
+                        if (ST) st.bc += branch_nibbles(dw);
+                        // Last wave of a non-final WG-stripe publishes its bottom row.
+                        if (w == W - 1 && sidx + 1 < a.NSW && lane < nstep) {
+                            const int v = xfer[((w + 1) * 2 + par) * CH + lane] - 64 * W * d;  // row-above domain
+                            const uint64_t gr = ((uint64_t)(uint32_t)(sidx + 1) << 32) | (uint32_t)v;
+                            __hip_atomic_store(gout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
+                    wg_barrier();
+                    if (sh_abort) break;
+                }
+            }
         }
         if (ST && real) {
             const bool rowok = jrow <= a.L2;
@@ -276,18 +315,36 @@ __global__ __launch_bounds__(64 * W) void nw_fill_kernel(FillArgs a) {
     }
 }
 
-// Boundary row/column seeding (computation.c:93-120): H[i][0] = -i*d,
-// H[0][j] = -j*d.  Directions of boundary cells are implicit.
-__global__ void nw_seed_kernel(int32_t* H, int64_t ldh, int32_t L1, int32_t L2, int32_t d) {
-    const int64_t n = (int64_t)L1 + 1 + L2;
+// Boundary row/column seeding (computation.c:93-120): row 0, H[i][0] = -i*d,
+// into row0[]; column 0, H[0][j] = -j*d, into slot i = 0 of every stripe.
+// Directions of boundary cells are implicit (code_at).
+__global__ void nw_seed_kernel(int32_t* row0, int32_t* tiles, int64_t spitch, int32_t L1, int32_t NG, int32_t d) {
+    const int64_t n = (int64_t)L1 + 1 + 64 * (int64_t)NG;
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n;
          x += (int64_t)gridDim.x * blockDim.x) {
-        if (x <= L1) H[x * ldh + PADROWS] = (int32_t)(-(int64_t)x * d);
+        if (x <= L1) row0[x] = (int32_t)(-x * (int64_t)d);
         else {
-            const int64_t j = x - L1;
-            H[PADROWS + j] = (int32_t)(-j * d);
+            const int64_t r = x - L1 - 1;          // = j - 1
+            tiles[(r >> 6) * spitch + (r & 63)] = (int32_t)(-(r + 1) * (int64_t)d);
         }
     }
+}
+
+__device__ __forceinline__ int32_t score_at(const int32_t* row0, const int32_t* tiles, int64_t spitch, int64_t i,
+                                            int64_t j) {
+    if (j == 0) return row0[i];
+    const int64_t r = j - 1;
+    return tiles[(r >> 6) * spitch + i * 64 + (r & 63)];
+}
+
+// Dense i-major copy of columns [i0, i1): out[(i-i0)*(L2+1) + j].
+__global__ void nw_gather_scores_kernel(const int32_t* row0, const int32_t* tiles, int64_t spitch, int32_t L2,
+                                        int64_t i0, int64_t i1, int32_t* out) {
+    const int64_t N = (int64_t)L2 + 1;
+    const int64_t n = (i1 - i0) * N;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n;
+         x += (int64_t)gridDim.x * blockDim.x)
+        out[x] = score_at(row0, tiles, spitch, i0 + x / N, x % N);
 }
 
 __device__ __forceinline__ uint32_t code_at(const uint32_t* D, int32_t NC, int64_t i, int64_t j) {
@@ -321,15 +378,15 @@ __global__ void nw_codes_kernel(const uint32_t* D, int32_t NC, int32_t L2, int64
 }
 
 // Per-column FNV-1a-64 of scores (int32 LE bytes) and codes (1 byte/cell).
-__global__ void nw_colhash_kernel(const int32_t* H, int64_t ldh, const uint32_t* D, int32_t NC, int32_t L1,
+__global__ void nw_colhash_kernel(const int32_t* row0, const int32_t* tiles, int64_t spitch, const uint32_t* D,
+                                  int32_t NC, int32_t L1,
                                   int32_t L2, uint64_t* hcol, uint64_t* dcol) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i > L1) return;
     const uint64_t P = 0x100000001b3ULL;
     uint64_t h = 0xcbf29ce484222325ULL, e = 0xcbf29ce484222325ULL;
-    const int32_t* col = H + i * ldh + PADROWS;
     for (int64_t j = 0; j <= L2; ++j) {
-        const uint32_t v = (uint32_t)col[j];
+        const uint32_t v = (uint32_t)score_at(row0, tiles, spitch, i, j);
         h = (h ^ (v & 0xff)) * P;
         h = (h ^ ((v >> 8) & 0xff)) * P;
         h = (h ^ ((v >> 16) & 0xff)) * P;
@@ -373,12 +430,14 @@ KernelFn pick_kernel(int W, bool sh, bool sd, bool stt) {
         case 4: return pick_flags<4>(sh, sd, stt);
         case 6: return pick_flags<6>(sh, sd, stt);
         case 8: return pick_flags<8>(sh, sd, stt);
-        case 16: return pick_flags<16>(sh, sd, stt);
+        case 12: return pick_flags<12>(sh, sd, stt);
+        case 15: return pick_flags<15>(sh, sd, stt);
         default: return nullptr;
     }
 }
 
-const int kWaveChoices[] = {1, 2, 4, 6, 8, 16};
+// Compute waves per workgroup (+1 loader wave; 16 waves = 1024 threads max).
+const int kWaveChoices[] = {1, 2, 4, 6, 8, 12, 15};
 
 int choose_waves(int64_t NG, int ncu) {
     if (const char* e = getenv("NW_WAVES")) {
@@ -404,11 +463,12 @@ struct nw_table {
     int64_t max_L1 = 0, max_L2 = 0;
     // geometry for the current sequences
     int64_t L1 = -1, L2 = -1;
-    int64_t NC = 0, NG = 0, ldh = 0;
+    int64_t NC = 0, NG = 0, spitch = 0;
     // device buffers
     uint8_t* s1 = nullptr;
     uint8_t* s2 = nullptr;
-    int32_t* H = nullptr;
+    int32_t* H = nullptr;       // score tiles
+    int32_t* row0 = nullptr;    // H[i][0]
     uint32_t* D = nullptr;
     int32_t* lastcol = nullptr;
     uint64_t* gran = nullptr;
@@ -448,6 +508,7 @@ void nw_table_destroy(nw_table* t) {
     (void)hipFree(t->s1);
     (void)hipFree(t->s2);
     (void)hipFree(t->H);
+    (void)hipFree(t->row0);
     (void)hipFree(t->D);
     (void)hipFree(t->lastcol);
     (void)hipFree(t->gran);
@@ -493,7 +554,6 @@ int nw_table_create(int device, int64_t max_L1, int64_t max_L2, uint32_t out_mas
 
     const int64_t NC = (max_L1 + CH - 1) / CH;
     const int64_t NG = (max_L2 + 63) / 64;
-    const int64_t ldh = 64 * (NG + 1);
     auto alloc = [&](void** p, size_t bytes) -> int {
         hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 256));
         if (e != hipSuccess)
@@ -504,12 +564,13 @@ int nw_table_create(int device, int64_t max_L1, int64_t max_L2, uint32_t out_mas
     if ((rc = alloc((void**)&t->s1, (size_t)(CH * NC + 64)))) return bail(rc);
     if ((rc = alloc((void**)&t->s2, (size_t)(64 * NG + 1024)))) return bail(rc);
     if (out_mask & NW_OUT_SCORES) {
-        if ((rc = alloc((void**)&t->H, (size_t)(max_L1 + 1) * (size_t)ldh * 4))) return bail(rc);
+        if ((rc = alloc((void**)&t->H, (size_t)std::max<int64_t>(NG, 1) * (size_t)(max_L1 + 1) * 256))) return bail(rc);
+        if ((rc = alloc((void**)&t->row0, (size_t)(max_L1 + 1) * 4))) return bail(rc);
     }
     if (out_mask & NW_OUT_DIRS) {
         if ((rc = alloc((void**)&t->D, (size_t)std::max<int64_t>(NG, 1) * std::max<int64_t>(NC, 1) * 256))) return bail(rc);
     }
-    if ((rc = alloc((void**)&t->lastcol, (size_t)ldh * 4))) return bail(rc);
+    if ((rc = alloc((void**)&t->lastcol, (size_t)(64 * NG + 128) * 4))) return bail(rc);
     // Granule slots: one per concurrently running WG-stripe + 1.
     const int64_t gpitch = CH * NC + CH;
     const int64_t nslot = 16 * (int64_t)t->ncu + 1;
@@ -528,7 +589,7 @@ int nw_table_set_sequences(nw_table* t, const char* s1, int64_t L1, const char* 
     t->L2 = L2;
     t->NC = (L1 + CH - 1) / CH;
     t->NG = (L2 + 63) / 64;
-    t->ldh = 64 * (t->NG + 1);
+    t->spitch = 64 * (L1 + 1);
     t->filled = false;
     const size_t n1 = (size_t)(CH * t->NC + 64), n2 = (size_t)(64 * t->NG + 1024);
     HIPCHK(hipMemsetAsync(t->s1, 0, n1, t->stream));
@@ -557,11 +618,7 @@ int nw_table_fill(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mas
     const int64_t L1 = t->L1, L2 = t->L2;
     HIPCHK(hipEventRecord(t->ev[0], t->stream));
     HIPCHK(hipMemsetAsync(t->ctl, 0, CTL_WORDS * 4, t->stream));
-    if (sh) nw_seed_kernel<<<256, 256, 0, t->stream>>>(t->H, t->ldh, (int32_t)L1, (int32_t)L2, d);
-    else if (L1 == 0) {
-        // score-only with no columns: the "last column" is column 0.
-        nw_seed_kernel<<<256, 256, 0, t->stream>>>(t->lastcol, t->ldh, 0, (int32_t)L2, d);
-    }
+    if (sh) nw_seed_kernel<<<256, 256, 0, t->stream>>>(t->row0, t->H, t->spitch, (int32_t)L1, (int32_t)t->NG, d);
     HIPCHK(hipGetLastError());
     int W = 0;
     if (L1 > 0 && L2 > 0) {
@@ -580,14 +637,14 @@ int nw_table_fill(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mas
         a.NG = (int32_t)t->NG;
         a.NSW = (int32_t)((t->NG + W - 1) / W);
         a.H = t->H;
-        a.ldh = t->ldh;
+        a.spitch = t->spitch;
         a.D = t->D;
         a.lastcol = t->lastcol;
         a.gran = t->gran;
         a.gpitch = CH * t->NC + CH;
         a.ctl = t->ctl;
         int occ = 1;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(fn), 64 * W, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(fn), 64 * (W + 1), 0));
         occ = std::max(occ, 1);
         const int64_t grid = std::min<int64_t>(a.NSW, (int64_t)t->ncu * std::min(occ, 16));
         a.nslot = (int32_t)std::min<int64_t>(grid + 1, (int64_t)(t->gran_bytes / 8 / a.gpitch));
@@ -596,7 +653,7 @@ int nw_table_fill(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mas
             HIPCHK(hipMemsetAsync(t->gran, 0, (size_t)a.nslot * a.gpitch * 8, t->stream));
         HIPCHK(hipEventRecord(t->ev[1], t->stream));
         void* kargs[] = {&a};
-        HIPCHK(hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3((unsigned)grid), dim3(64 * W), kargs, 0,
+        HIPCHK(hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3((unsigned)grid), dim3(64 * (W + 1)), kargs, 0,
                                t->stream));
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(t->ev[2], t->stream));
@@ -609,7 +666,8 @@ int nw_table_fill(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mas
     HIPCHK(hipMemcpyAsync(ctl, t->ctl, sizeof ctl, hipMemcpyDeviceToHost, t->stream));
     int32_t corner = 0;
     if (L1 > 0 && L2 > 0) {
-        const int32_t* src = sh ? t->H + L1 * t->ldh + PADROWS + L2 : t->lastcol + PADROWS + L2;
+        const int64_t r = L2 - 1;
+        const int32_t* src = sh ? t->H + (r >> 6) * t->spitch + L1 * 64 + (r & 63) : t->lastcol + L2;
         HIPCHK(hipMemcpyAsync(&corner, src, 4, hipMemcpyDeviceToHost, t->stream));
     }
     HIPCHK(hipStreamSynchronize(t->stream));
@@ -645,14 +703,26 @@ int nw_table_elapsed_ms(nw_table* t, float* kernel_ms, float* call_ms) {
     return NW_OK;
 }
 
-int64_t nw_table_score_pitch(const nw_table* t) { return t ? t->ldh : 0; }
+int64_t nw_table_score_pitch(const nw_table* t) { return t ? t->spitch : 0; }
 int nw_table_waves(const nw_table* t) { return t ? t->waves : 0; }
 
 static int copy_scores_impl(nw_table* t, int64_t i0, int64_t i1, int32_t* dst) {
     const int64_t N = t->L2 + 1;
-    HIPCHK(hipMemcpy2DAsync(dst, (size_t)N * 4, t->H + i0 * t->ldh + PADROWS, (size_t)t->ldh * 4, (size_t)N * 4,
-                            (size_t)(i1 - i0), hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    // Gather the tiles into dense columns through a bounded staging buffer.
+    const int64_t cols_per = std::max<int64_t>(1, ((int64_t)256 << 20) / (4 * N));
+    int32_t* stage = nullptr;
+    HIPCHK(hipMalloc(&stage, (size_t)(std::min(cols_per, i1 - i0) * N * 4)));
+    hipError_t e = hipSuccess;
+    for (int64_t c0 = i0; c0 < i1 && e == hipSuccess; c0 += cols_per) {
+        const int64_t c1 = std::min(i1, c0 + cols_per);
+        nw_gather_scores_kernel<<<1024, 256, 0, t->stream>>>(t->row0, t->H, t->spitch, (int32_t)t->L2, c0, c1, stage);
+        e = hipGetLastError();
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(dst + (c0 - i0) * N, stage, (size_t)((c1 - c0) * N * 4), hipMemcpyDeviceToHost, t->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(t->stream);
+    }
+    (void)hipFree(stage);
+    if (e != hipSuccess) return fail(NW_ERR_HIP, std::string("nw_table_copy_scores: ") + hipGetErrorString(e));
     return NW_OK;
 }
 
@@ -674,7 +744,7 @@ int nw_table_copy_last_column(nw_table* t, int32_t* dst) {
         for (int64_t j = 0; j <= t->L2; ++j) dst[j] = (int32_t)(-(t->L1 + j) * (int64_t)t->last_d);
         return NW_OK;
     }
-    HIPCHK(hipMemcpyAsync(dst + 1, t->lastcol + PADROWS + 1, (size_t)t->L2 * 4, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(dst + 1, t->lastcol + 1, (size_t)t->L2 * 4, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipStreamSynchronize(t->stream));
     dst[0] = (int32_t)(-t->L1 * (int64_t)t->last_d);
     return NW_OK;
@@ -707,7 +777,7 @@ int nw_table_hash(nw_table* t, uint64_t* hH, uint64_t* hD) {
     HIPCHK(hipMalloc(&dh, (size_t)ncol * 16));
     const bool have_d = (t->last_mask & NW_OUT_DIRS) != 0;
     nw_colhash_kernel<<<(unsigned)((ncol + 255) / 256), 256, 0, t->stream>>>(
-        t->H, t->ldh, have_d ? t->D : nullptr, (int32_t)t->NC, (int32_t)t->L1, (int32_t)t->L2, dh, dh + ncol);
+        t->row0, t->H, t->spitch, have_d ? t->D : nullptr, (int32_t)t->NC, (int32_t)t->L1, (int32_t)t->L2, dh, dh + ncol);
     std::vector<uint64_t> hv((size_t)ncol * 2);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(hv.data(), dh, (size_t)ncol * 16, hipMemcpyDeviceToHost, t->stream);

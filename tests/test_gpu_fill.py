@@ -68,7 +68,7 @@ def test_params_vs_oracle(m, k, d):
     _check_against_oracle(O.gen_dna(3, 700), O.gen_dna(4, 900), m, k, d)
 
 
-@pytest.mark.parametrize("w", [1, 2, 4, 6, 8, 16])
+@pytest.mark.parametrize("w", [1, 2, 4, 6, 8, 12, 15])
 def test_every_workgroup_height(waves, w):
     """Each WG height; L2 spans many WG-stripes so the granule hand-off runs."""
     waves(w)
@@ -156,3 +156,29 @@ def test_10k_config_c2(ref_kats):
         D = t.codes()
     assert "%016x" % O.fnv(H) == case["hH"]
     assert "%016x" % O.fnv(D) == case["hD"]
+
+
+def test_100k_config_c3_colchain():
+    """configs[2]: 100k x 100k, full table in HBM.  The reference cannot run it
+    (1.36 TB); parity is transitive through the oracle-generated
+    tests/golden/big_colchain.json (the oracle is pinned to the reference up to
+    10k x 10k by tests/test_oracle_golden.py).  Also the size-independent
+    properties: score-only corner/last column == full-table ones, refill
+    idempotent."""
+    from conftest import load_golden
+    g = load_golden("big_colchain.json")[0]
+    s1, s2 = nw_amd.gen_dna(1, g["L1"]), nw_amd.gen_dna(2, g["L2"])
+    with nw_amd.Table(g["L1"], g["L2"]) as t:
+        t.set_sequences(s1, s2)
+        t.fill(g["m"], g["k"], g["d"], ALL)
+        st = t.stats()
+        assert (st.corner, st.greatest_abs_interior, st.branch_count) == \
+            (g["corner"], g["gav"], g["branch_count"])
+        hH, hD = t.hash()
+        assert ("%016x" % hH, "%016x" % hD) == (g["hH2"], g["hD2"])
+        last = t.last_column()
+        t.fill(g["m"], g["k"], g["d"], nw_amd.NW_OUT_STATS)      # score-only
+        st2 = t.stats()
+        assert (st2.corner, st2.greatest_abs_interior, st2.branch_count) == \
+            (g["corner"], g["gav"], g["branch_count"])
+        assert np.array_equal(t.last_column(), last)
