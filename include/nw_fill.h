@@ -89,11 +89,12 @@ int nw_fill(const char *s1, int64_t L1, const char *s2, int64_t L2,
  * Device-resident table (the 100k x 100k path: the 45 GB table stays in HBM).
  *
  * Device layout (DESIGN.md "Data layout in HBM"):
- *   scores: stripe-major tiles.  Rows j >= 1 are grouped in 64-row stripes
- *           g = (j-1)/64, lane l = (j-1)%64; cell (i, j) is element
- *           g*P + i*64 + l with P = nw_table_score_pitch() = (L1+1)*64, so one
- *           column of one stripe is 256 contiguous bytes and a stripe's columns
- *           follow each other.  Row 0 (H[i][0] = -i*d) is kept apart.
+ *   scores: stripe-major quad tiles.  Row 0 and column 0 (the seeds
+ *           -i*d, -j*d) are not stored.  Interior cell (i, j) has stripe
+ *           g = (j-1)/64, lane l = (j-1)%64, column quad q = (i-1)/4,
+ *           r = (i-1)%4 and is element g*P + (q*64 + l)*4 + r with
+ *           P = nw_table_score_pitch() = 512*NQ: a lane's 4 consecutive
+ *           columns form one 16-byte word, one quad of a stripe is 1 KB.
  *   dirs  : 32-bit words, one per (64-row stripe g, 8-column group q, lane l):
  *           word (g*NQ + q)*64 + l, NQ = ceil(L1/8), holds the codes of cells
  *           (i = 8q+1+s, j = 64g+1+l), s = 0..7, code s in bits [28-4s, 31-4s].
@@ -134,6 +135,12 @@ int nw_table_copy_codes(nw_table *t, int64_t i0, int64_t i1, uint8_t *dst);
 int nw_table_copy_last_column(nw_table *t, int32_t *dst);
 /* Geometry of the device layout (for zero-copy consumers). */
 int64_t nw_table_score_pitch(const nw_table *t);
+/* In-kernel timeline of the last fill, recorded only when $NW_TRACE is set
+ * (s_memrealtime, 100 MHz): 4 words per workgroup stripe s -- [4s] dequeued,
+ * [4s+1] first chunk started, [4s+2] last wave finished, [4s+3] blockIdx |
+ * hardware CU id << 32.  Copies min(n, total) words into dst (if non-NULL)
+ * and returns the total word count (0 when no trace was recorded). */
+int64_t nw_table_trace(nw_table *t, uint64_t *dst, int64_t n);
 /* Waves per workgroup chosen for the last fill (tuning / reporting). */
 int nw_table_waves(const nw_table *t);
 

@@ -53,14 +53,15 @@ struct FillArgs {
     int32_t NC;             // chunks = ceil(L1 / 8)
     int32_t NG;             // wave stripes = ceil(L2 / 64)
     int32_t NSW;            // workgroup stripes = ceil(NG / W)
-    int32_t* H;             // score tiles: (i, j>=1) at H[(g*(L1+1) + i)*64 + l], j-1 = 64g+l
-    int64_t spitch;         // (L1+1)*64: elements per stripe
+    int32_t* H;             // score tiles, see score_at()
+    int64_t spitch;         // 512*NC: elements per 64-row stripe
     uint32_t* D;            // codes: word ((g*NC + q)*64 + lane)
     int32_t* lastcol;       // score-only: H[L1][j] at lastcol[63 + j]
     uint64_t* gran;         // boundary granules, slot s at gran + s*gpitch
     int64_t gpitch;
     int32_t nslot;
     uint32_t* ctl;          // CtlWord
+    uint64_t* trace;        // optional timeline: 4 words per WG-stripe (see nw_table_trace)
 };
 
 // ---------------------------------------------------------------- DPP helpers
@@ -69,21 +70,12 @@ __device__ __forceinline__ int wave_shr1(int old, int v) {
     return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xf, 0xf, false);
 }
 
-// Inclusive prefix max over the 64 lanes (lane l gets max of lanes 0..l).
-// Out-of-row sources leave the lane unchanged (bound_ctrl off), which is the
-// identity for max; the compiler fuses each step into one v_max_i32_dpp.
-__device__ __forceinline__ int wave_prefix_max(int y) {
-    constexpr int NEG = (int)0x80000000;
-    y = max(y, __builtin_amdgcn_update_dpp(NEG, y, 0x111, 0xf, 0xf, false));  // row_shr:1
-    y = max(y, __builtin_amdgcn_update_dpp(NEG, y, 0x112, 0xf, 0xf, false));  // row_shr:2
-    y = max(y, __builtin_amdgcn_update_dpp(NEG, y, 0x114, 0xf, 0xf, false));  // row_shr:4
-    y = max(y, __builtin_amdgcn_update_dpp(NEG, y, 0x118, 0xf, 0xf, false));  // row_shr:8
-    y = max(y, __builtin_amdgcn_update_dpp(NEG, y, 0x142, 0xa, 0xf, false));  // row_bcast:15
-    y = max(y, __builtin_amdgcn_update_dpp(NEG, y, 0x143, 0xc, 0xf, false));  // row_bcast:31
-    return y;
-}
-
 typedef const __attribute__((address_space(4))) uint64_t* cptr64;
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4_t u32x4(int a, int b, int c, int d) {
+    return u32x4_t{(unsigned)a, (unsigned)b, (unsigned)c, (unsigned)d};
+}
 
 __device__ __forceinline__ int iabs(int v) { return v < 0 ? -v : v; }
 
@@ -92,11 +84,6 @@ __device__ __forceinline__ uint32_t branch_nibbles(uint32_t x) {
     uint32_t y = (x & (x >> 1)) | (x & (x >> 2)) | ((x >> 1) & (x >> 2));
     return __builtin_popcount(y & 0x11111111u);
 }
-
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
-// (lgkmcnt) and syncs.  Unlike __syncthreads() it carries no fence, so it
-// never waits for the wave's in-flight global stores (vmcnt).
-__device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Wave-uniform copies of per-wave values (so address math stays scalar).
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -113,61 +100,180 @@ struct WaveState {
 
 // One 8-column chunk of one wave.  NSTEP is 8 except for the last chunk.
 // Cell recurrence = needleman-wunsch.c:429-465; direction flags :485-503.
+// ----------------------------------------------------------- step kernels
+// One column step of one wave, hand-scheduled.  The loop-carried chain is
+//   G --dpp wave_shr:1--> sh --add--> dg --max3(lf,dg,top)--> Y --6 x dpp max--> G'
+// and every DPP read of a VGPR written by the previous VALU needs two wait
+// states.  Instead of s_nop, those slots carry the *previous* step's
+// independent outputs: its direction code (3 compares, shifted into `acc`
+// with v_addc: acc = 16*acc + diag + 2*up + 4*left), its score H = G - laneoff
+// and (stats) the running max |H|.  The previous step's up candidate is this
+// step's `sh` (wave_shr:1 of G with lane 0 = row above), so it comes free.
+#define NW_STEP_HEAD                                                   \
+    "v_cmp_eq_u32_e32 vcc, %[ch], %[c2]\n\t"                           \
+    "v_cndmask_b32_e32 %[sub], %[ck], %[cm], vcc\n\t"                  \
+    "v_mov_b32_dpp %[sh], %[G] wave_shr:1 row_mask:0xf bank_mask:0xf\n\t" \
+    "v_subrev_u32_e32 %[lf], %[d], %[G]\n\t"                           \
+    "v_add_u32_e32 %[dg], %[sh], %[sub]\n\t"                           \
+    "v_max3_i32 %[Y], %[lf], %[dg], %[top]\n\t"
+#define NW_DPP(CTRL) "v_max_i32_dpp %[Y], %[Y], %[Y] " CTRL "\n\t"
+#define NW_FILL_A                                                      \
+    "v_cmp_eq_i32_e64 %[sa], %[pG], %[pdg]\n\t"                        \
+    "v_cmp_eq_i32_e64 %[sb], %[pG], %[sh]\n\t"
+#define NW_FILL_B                                                      \
+    "v_cmp_eq_i32_e32 vcc, %[pG], %[plf]\n\t"                          \
+    "v_lshlrev_b32_e32 %[acc], 1, %[acc]\n\t"
+#define NW_FILL_C                                                      \
+    "v_addc_co_u32_e64 %[acc], %[junk], %[acc], %[acc], vcc\n\t"       \
+    "v_addc_co_u32_e64 %[acc], %[junk], %[acc], %[acc], %[sb]\n\t"
+#define NW_FILL_D                                                      \
+    "v_addc_co_u32_e64 %[acc], %[junk], %[acc], %[acc], %[sa]\n\t"     \
+    "v_sub_u32_e32 %[Hp], %[pG], %[lo]\n\t"
+#define NW_FILL_E                                                      \
+    "v_sub_u32_e32 %[tmp], 0, %[Hp]\n\t"                               \
+    "v_max3_i32 %[gav], %[gav], %[Hp], %[tmp]\n\t"
+#define NW_NOP2 "s_nop 1\n\t"
+#define NW_SCAN_FILLED(E)                                              \
+    NW_FILL_A NW_DPP("row_shr:1 row_mask:0xf bank_mask:0xf")           \
+    NW_FILL_B NW_DPP("row_shr:2 row_mask:0xf bank_mask:0xf")           \
+    NW_FILL_C NW_DPP("row_shr:4 row_mask:0xf bank_mask:0xf")           \
+    NW_FILL_D NW_DPP("row_shr:8 row_mask:0xf bank_mask:0xf")           \
+    E         NW_DPP("row_bcast:15 row_mask:0xa bank_mask:0xf")        \
+    NW_NOP2   "v_max_i32_dpp %[Y], %[Y], %[Y] row_bcast:31 row_mask:0xc bank_mask:0xf"
+#define NW_SCAN_BARE                                                   \
+    NW_NOP2 NW_DPP("row_shr:1 row_mask:0xf bank_mask:0xf")             \
+    NW_NOP2 NW_DPP("row_shr:2 row_mask:0xf bank_mask:0xf")             \
+    NW_NOP2 NW_DPP("row_shr:4 row_mask:0xf bank_mask:0xf")             \
+    NW_NOP2 NW_DPP("row_shr:8 row_mask:0xf bank_mask:0xf")             \
+    NW_NOP2 NW_DPP("row_bcast:15 row_mask:0xa bank_mask:0xf")          \
+    NW_NOP2 "v_max_i32_dpp %[Y], %[Y], %[Y] row_bcast:31 row_mask:0xc bank_mask:0xf"
+
+struct StepIO {
+    int G, sh, dg, lf;      // this step: new G (out), shift / diag / left candidates
+    int pG, pdg, plf;       // previous step (inputs of the filled outputs)
+    int Hp;                 // previous step's score (out)
+    uint32_t acc;           // direction codes accumulator
+    int gav;                // running max |H|
+};
+
+// MODE 0: first step of a chunk (nothing pending), 1: fill with the previous
+// step's code + score, 2: also its |H| for the stats.
+template <int MODE>
+__device__ __forceinline__ void step_asm(StepIO& io, int Tprev, int top, uint32_t ch, uint32_t c2, int vck, int vcm,
+                                         int d, int laneoff) {
+    int Y, sub, tmp;
+    uint64_t sa, sb, junk;
+    int sh = Tprev;  // DPP lane 0 keeps the old value: the row above
+#define NW_OPERANDS                                                                              \
+    : [Y] "=&v"(Y), [sh] "+v"(sh), [sub] "=&v"(sub), [dg] "=&v"(io.dg), [lf] "=&v"(io.lf),        \
+      [Hp] "=&v"(io.Hp), [acc] "+v"(io.acc), [gav] "+v"(io.gav), [tmp] "=&v"(tmp), [sa] "=&s"(sa), \
+      [sb] "=&s"(sb), [junk] "=&s"(junk)                                                          \
+    : [G] "v"(io.G), [ch] "s"(ch), [c2] "v"(c2), [ck] "v"(vck), [cm] "v"(vcm), [d] "s"(d),       \
+      [top] "v"(top), [pG] "v"(io.pG), [pdg] "v"(io.pdg), [plf] "v"(io.plf), [lo] "v"(laneoff)    \
+    : "vcc"
+    if constexpr (MODE == 0) {
+        asm volatile(NW_STEP_HEAD NW_SCAN_BARE NW_OPERANDS);
+    } else if constexpr (MODE == 1) {
+        asm volatile(NW_STEP_HEAD NW_SCAN_FILLED(NW_NOP2) NW_OPERANDS);
+    } else {
+        asm volatile(NW_STEP_HEAD NW_SCAN_FILLED(NW_FILL_E) NW_OPERANDS);
+    }
+#undef NW_OPERANDS
+    io.sh = sh;
+    io.G = Y;
+}
+
+// One 8-column chunk of one wave.  NSTEP is 8 except for the last chunk.
+// Cell recurrence = needleman-wunsch.c:429-465; direction flags :485-503.
+// In the shifted domain G = H + r*d each column is a prefix max over lanes:
+//     G_i = prefmax( max(G_{i-1} - d, G_{i-1}[l-1] + sub_i, T_i) ).
 template <bool SH, bool SD, bool ST, bool LAST>
-__device__ __forceinline__ void chunk_body(const FillArgs& a, WaveState& st, const int* T,
-                                           int c, int nstep, int lane, int64_t tile_off, int j0,
-                                           int d, int vcm, int vck, int* bot_wr, uint32_t* dword_out) {
-    // s1[8c .. 8c+7]: one uniform 8-byte load through the constant address
-    // space -> s_load_dwordx2 (lgkmcnt), never a vector load that would make
-    // the wave wait for its own in-flight score stores.
-    const uint64_t ch8 = *(cptr64)(a.s1 + 8 * (int64_t)c);
-    uint32_t acc = 0;
-    // Buffer descriptor on this chunk's 8 column segments (2 KB contiguous in
-    // the stripe-major tile layout): per-step addresses are lane*4 (VGPR) +
-    // s*256 (SGPR) -- no VALU address math.
-    int32_t* cb = a.H + tile_off + (int64_t)(8 * c + 1) * 64;
+__device__ __forceinline__ void chunk_body(const FillArgs& a, WaveState& st, const int* T, uint64_t ch8, int c,
+                                           int nstep, int lane, int64_t tile_off, int j0, int d, int vcm, int vck,
+                                           int* bot_wr, uint32_t* dword_out) {
+    // Buffer descriptor on this chunk's two column quads (2 KB contiguous in
+    // the stripe-major quad layout): lane l stores its 4 consecutive columns
+    // as one 16-byte buffer_store_dwordx4 at lane*16 (+1024 for the 2nd quad).
+    int32_t* cb = a.H + tile_off + (int64_t)c * 512;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(cb, 0, 0x7fffffff, 0x00020000);
+    StepIO io;
+    io.G = st.G;
+    io.acc = 0;
+    io.gav = st.gav;
+    io.pG = io.pdg = io.plf = 0;
+    int Tprev = st.Tprev;
+    int h[CH];
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
         if (LAST && s >= nstep) break;
         const uint32_t ch = (uint32_t)(ch8 >> (8 * s)) & 0xffu;
-        const int sub = (ch == st.c2) ? vcm : vck;        // m+d or d-k
-        const int sh = wave_shr1(st.Tprev, st.G);         // G[l-1], lane 0: row above
-        const int dg = sh + sub;                          // diag candidate (shifted)
-        const int lf = st.G - d;                          // left candidate (shifted)
-        const int top = T[s];                             // up candidate of lane 0
-        const int Y = max(max(lf, dg), top);
-        const int G = wave_prefix_max(Y);                 // resolves all "up" terms
-        const int Hv = G - st.laneoff;
-        if (SH) __builtin_amdgcn_raw_buffer_store_b32(Hv, rs, lane * 4, s * 256, 0);
-        if (SD || ST) {                                   // codes also feed branch_count
-            const int up = wave_shr1(top, G);             // up candidate (shifted)
-            acc = (acc << 4) | (uint32_t)(G == dg) | ((uint32_t)(G == up) << 1) |
-                  ((uint32_t)(G == lf) << 2);
-        }
-        if (ST) st.gav = max(st.gav, iabs(Hv));
-        bot_wr[s] = G;   // lane 63 -> bottom-row slot, lanes 0..62 -> scratch
-        st.G = G;
-        st.Tprev = top;
-        if (LAST && !SH && s == nstep - 1) {
-            // score-only: keep the last column H[L1][*].
-            a.lastcol[j0 + lane] = Hv;
+        if (s == 0) step_asm<0>(io, Tprev, T[s], ch, st.c2, vck, vcm, d, st.laneoff);
+        else if (ST) step_asm<2>(io, Tprev, T[s], ch, st.c2, vck, vcm, d, st.laneoff);
+        else step_asm<1>(io, Tprev, T[s], ch, st.c2, vck, vcm, d, st.laneoff);
+        if (s > 0) h[s - 1] = io.Hp;
+        if (SH && !LAST && s == 4)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4(h[0], h[1], h[2], h[3]), rs, lane * 16, 0, 0);
+        bot_wr[s] = io.G;   // lane 63 -> bottom-row slot, lanes 0..62 -> scratch
+        io.pG = io.G;
+        io.pdg = io.dg;
+        io.plf = io.lf;
+        Tprev = T[s];
+    }
+    // Outputs of the chunk's last step (not overlapped).
+    const int slast = LAST ? nstep - 1 : CH - 1;
+    const int up = wave_shr1(Tprev, io.G);
+    const int Hv = io.G - st.laneoff;
+    h[slast] = Hv;
+    if (SH) {
+        if (LAST) {
+            // partial chunk: unused slots land in the quad padding
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4(h[0], nstep > 1 ? h[1] : 0, nstep > 2 ? h[2] : 0,
+                                                             nstep > 3 ? h[3] : 0), rs, lane * 16, 0, 0);
+            if (nstep > 4)
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4(h[4], nstep > 5 ? h[5] : 0, nstep > 6 ? h[6] : 0,
+                                                                 nstep > 7 ? h[7] : 0), rs, lane * 16 + 1024, 0, 0);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4(h[4], h[5], h[6], h[7]), rs, lane * 16 + 1024, 0, 0);
         }
     }
+    uint32_t acc = (io.acc << 4) | (uint32_t)(io.G == io.dg) | ((uint32_t)(io.G == up) << 1) |
+                   ((uint32_t)(io.G == io.lf) << 2);
+    if (ST) io.gav = max(io.gav, iabs(Hv));
+    if (LAST && !SH) a.lastcol[j0 + lane] = Hv;            // score-only: H[L1][*]
     if (LAST && nstep < CH) acc <<= 4 * (CH - nstep);
+    st.G = io.G;
+    st.Tprev = Tprev;
+    st.gav = io.gav;
     *dword_out = acc;
 }
 
-// Workgroup = W compute waves (64-row stripes, stacked) + 1 loader wave.
-// The loader feeds the top row of the WG-stripe for chunk t+1 into LDS while
-// the compute waves run superstep t; it issues no stores, so its waits on
-// the hand-off loads are exact, and the compute waves never wait on vmcnt.
+// LDS counters of the barrier-free intra-workgroup pipeline.
+__device__ __forceinline__ int lds_ld(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_publish(int* p, int v) {
+    // Every LDS write this wave issued before (ring data) completes first:
+    // LDS is in-order per wave, and the wait makes the counter the last word.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Workgroup = W compute waves (64-row stripes, stacked) + 1 loader wave, no
+// barriers inside a stripe.  Wave w takes the top row of each 8-column chunk
+// from an LDS ring tring[w] (R chunk slots) filled by its producer (the
+// loader for w = 0, wave w-1 otherwise) and puts its own bottom row into
+// tring[w+1].  prog[w] = chunks available in tring[w], cons[w] = chunks wave w
+// has taken out of it; a producer only waits when it is R chunks ahead.
+// The loader feeds tring[0] from the previous WG-stripe's granules; it issues
+// no stores, so its waits on the hand-off loads are exact, and the compute
+// waves never wait on vmcnt.
 template <int W, bool SH, bool SD, bool ST>
 __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
-    // xfer[w][par][8]: top row of wave w (w = 0: from the loader, else the
-    // bottom row of wave w-1) for chunk parity par.  Then 72 scratch dwords.
-    constexpr int XFER = (W + 1) * 2 * CH;
-    __shared__ __attribute__((aligned(16))) int xfer[XFER + 64 + CH];
+    constexpr int R = 4;
+    __shared__ __attribute__((aligned(16))) int tring[(W + 1) * R * CH];
+    __shared__ int scratch[64 + CH];
+    __shared__ int prog[W + 1];
+    __shared__ int cons[W + 1];
     __shared__ int sh_sidx;
     __shared__ int sh_abort;
 
@@ -186,117 +292,147 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             sh_sidx = (int)atomicAdd(&a.ctl[CTL_NEXT], 1u);
             sh_abort = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
         }
+        if (threadIdx.x <= W) {
+            prog[threadIdx.x] = 0;
+            cons[threadIdx.x] = 0;
+        }
         __syncthreads();
         const int sidx = uni(sh_sidx);
         if (sidx >= a.NSW || sh_abort) break;
+        if (a.trace && threadIdx.x == 0) {
+            a.trace[4 * (int64_t)sidx + 0] = __builtin_amdgcn_s_memrealtime();
+            a.trace[4 * (int64_t)sidx + 3] = (uint64_t)blockIdx.x | ((uint64_t)__smid() << 32);
+        }
 
         const int g = sidx * W + w;                // wave stripe (compute waves)
         const bool real = !loader && g < a.NG;
+        const bool next_real = !loader && w + 1 < W && g + 1 < a.NG;
         const int j0 = 1 + 64 * g;                 // first row of the wave stripe
         const int jrow = j0 + lane;
-        const int64_t tile_off = (int64_t)g * a.spitch;
         WaveState st;
-        st.c2 = real ? a.s2[jrow - 1] : 0u;
-        st.laneoff = (64 * w + lane) * d;
-        // column 0: H[0][j] = -j*d  ->  G = -(1 + 64*sidx*W)*d for every lane.
-        st.G = -(1 + 64 * sidx * W) * d;
-        st.Tprev = st.G;
+        st.G = 0;
         st.gav = 0;
         st.bc = 0;
 
-        // ---- loader state: top row of this WG-stripe, one chunk ahead ----
-        const uint64_t* gin = a.gran + (int64_t)(sidx % a.nslot) * a.gpitch;
-        uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
-        uint64_t pf = 0;
-        // Fill xfer[0][par(c)] with chunk c's top values (G domain of row "-1").
-        auto loader_fill = [&](int c) {
-            int* dst = &xfer[(c & 1) * CH];
-            const int n = (c == NC - 1) ? nlast : CH;
-            if (sidx == 0) {
-                // row 0: H[i][0] - d = -(i+1)*d   (computation.c:102-110)
-                if (lane < CH) dst[lane] = -(CH * c + 2 + lane) * d;
-                return;
-            }
-            const uint32_t want = (uint32_t)sidx;
-            bool ok = lane >= n || (uint32_t)(pf >> 32) == want;
-            if (!__all(ok)) {
-                const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-                for (;;) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (!ok)
-                        pf = __hip_atomic_load(gin + CH * (int64_t)c + lane, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                    ok = lane >= n || (uint32_t)(pf >> 32) == want;
-                    if (__all(ok)) break;
-                    const int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
-                    const uint32_t ab = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
-                    if (ab || now - t0 > SPIN_TICKS) {
-                        if (lane == 0) {
-                            __hip_atomic_store(&a.ctl[CTL_ABORT], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            if (!ab) atomicCAS(&a.ctl[CTL_ERR], 0u, (uint32_t)NW_ERR_TIMEOUT);
-                            sh_abort = 1;
-                        }
-                        break;
-                    }
-                }
-            }
-            if (lane < CH) dst[lane] = (int)(uint32_t)pf;
-            if (c + 1 < NC && lane < CH)          // prefetch the next chunk
-                pf = __hip_atomic_load(gin + CH * (int64_t)(c + 1) + lane, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-        };
         if (loader) {
             // ---------------- loader wave: no stores, exact waits ----------------
+            const uint64_t* gin = a.gran + (int64_t)(sidx % a.nslot) * a.gpitch;
+            uint64_t pf = 0;
             if (sidx > 0 && lane < CH)
                 pf = __hip_atomic_load(gin + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            loader_fill(0);
-            wg_barrier();
-            if (!sh_abort) {
-                const int nsuper = NC + W - 1;
-                for (int t = 0; t < nsuper; ++t) {
-                    if (t + 1 < NC) loader_fill(t + 1);
-                    wg_barrier();
-                    if (sh_abort) break;
-                }
-            }
-        } else {
-            // ---------------- compute waves: one chunk per superstep ------------
-            wg_barrier();
-            if (!sh_abort) {
-                const int nsuper = NC + W - 1;
-                for (int t = 0; t < nsuper; ++t) {
-                    const int c = t - w;
-                    if (real && c >= 0 && c < NC) {
-                        const int par = c & 1;
-                        const int* top_lds = &xfer[(w * 2 + par) * CH];
-                        // Bottom row goes to xfer[w+1][par]; lanes 0..62 hit scratch.
-                        int* bot_wr = (lane == 63) ? &xfer[((w + 1) * 2 + par) * CH] : &xfer[XFER + lane];
-                        const int nstep = (c == NC - 1) ? nlast : CH;
-                        const int4 t03 = *reinterpret_cast<const int4*>(top_lds);
-                        const int4 t47 = *reinterpret_cast<const int4*>(top_lds + 4);
-                        const int T[CH] = {t03.x, t03.y, t03.z, t03.w, t47.x, t47.y, t47.z, t47.w};
-                        uint32_t dw;
-                        if (c == NC - 1)
-                            chunk_body<SH, SD, ST, true>(a, st, T, c, nstep, lane, tile_off, j0, d, vcm, vck, bot_wr, &dw);
-                        else
-                            chunk_body<SH, SD, ST, false>(a, st, T, c, CH, lane, tile_off, j0, d, vcm, vck, bot_wr, &dw);
-                        if (jrow > a.L2) dw = 0;
-                        if (SD) a.D[((int64_t)g * NC + c) * 64 + lane] = dw;
-                        if (ST) st.bc += branch_nibbles(dw);
-                        // Last wave of a non-final WG-stripe publishes its bottom row.
-                        if (w == W - 1 && sidx + 1 < a.NSW && lane < nstep) {
-                            const int v = xfer[((w + 1) * 2 + par) * CH + lane] - 64 * W * d;  // row-above domain
-                            const uint64_t gr = ((uint64_t)(uint32_t)(sidx + 1) << 32) | (uint32_t)v;
-                            __hip_atomic_store(gout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
+            for (int c = 0; c < NC; ++c) {
+                const int n = (c == NC - 1) ? nlast : CH;
+                while (lds_ld(&cons[0]) < c - R + 1) __builtin_amdgcn_s_sleep(1);   // ring slot free?
+                int* dst = &tring[(c % R) * CH];
+                if (sidx == 0) {
+                    // row 0: H[i][0] - d = -(i+1)*d   (computation.c:102-110)
+                    if (lane < CH) dst[lane] = -(CH * c + 2 + lane) * d;
+                } else {
+                    const uint32_t want = (uint32_t)sidx;
+                    bool ok = lane >= n || (uint32_t)(pf >> 32) == want;
+                    if (!__all(ok)) {
+                        const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+                        for (;;) {
+                            __builtin_amdgcn_s_sleep(1);
+                            if (!ok)
+                                pf = __hip_atomic_load(gin + CH * (int64_t)c + lane, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                            ok = lane >= n || (uint32_t)(pf >> 32) == want;
+                            if (__all(ok)) break;
+                            const int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
+                            const uint32_t ab = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT);
+                            if (ab || now - t0 > SPIN_TICKS) {
+                                if (lane == 0) {
+                                    __hip_atomic_store(&a.ctl[CTL_ABORT], 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                                    if (!ab) atomicCAS(&a.ctl[CTL_ERR], 0u, (uint32_t)NW_ERR_TIMEOUT);
+                                    __hip_atomic_store(&sh_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                }
+                                break;
+                            }
                         }
                     }
-                    wg_barrier();
-                    if (sh_abort) break;
+                    if (lds_ld(&sh_abort)) break;
+                    if (lane < CH) dst[lane] = (int)(uint32_t)pf;
+                    if (c + 1 < NC && lane < CH)          // prefetch the next chunk
+                        pf = __hip_atomic_load(gin + CH * (int64_t)(c + 1) + lane, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (lane == 0) lds_publish(&prog[0], c + 1);
+            }
+        } else if (real) {
+            // ---------------- compute wave: its 64-row stripe, chunk by chunk ----
+            uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
+            const int64_t tile_off = (int64_t)g * a.spitch;
+            st.c2 = a.s2[jrow - 1];
+            st.laneoff = (64 * w + lane) * d;
+            // column 0: H[0][j] = -j*d  ->  G = -(1 + 64*sidx*W)*d for every lane.
+            st.G = -(1 + 64 * sidx * W) * d;
+            st.Tprev = st.G;
+            const bool publish = (w == W - 1) && sidx + 1 < a.NSW;
+            const int* tin = &tring[w * R * CH];
+            if (a.trace && lane == 0 && w == 0) a.trace[4 * (int64_t)sidx + 1] = __builtin_amdgcn_s_memrealtime();
+            // Chunk prologue, software-pipelined one chunk ahead: the s1 bytes
+            // (s_load), our producer's progress, the ring slot and our
+            // consumer's progress for chunk c+1 are all requested at the start
+            // of chunk c and only checked at its end.  LDS is in order per
+            // wave, so ring data read after a progress value that covers it is
+            // valid.  (s_load shares lgkmcnt with LDS, so it is issued first.)
+            uint64_t ch8 = *(cptr64)(a.s1);
+            int pin = lds_ld(&prog[w]);
+            int4 t03 = *reinterpret_cast<const int4*>(&tin[0]);
+            int4 t47 = *reinterpret_cast<const int4*>(&tin[4]);
+            int pout = next_real ? lds_ld(&cons[w + 1]) : (1 << 30);
+            for (int c = 0; c < NC; ++c) {
+                const int slot = (c % R) * CH;
+                if (pin <= c || pout < c - R + 1) {
+                    // slow path: producer behind (or ring full) -- wait, then re-read
+                    for (;;) {
+                        pin = lds_ld(&prog[w]);
+                        pout = next_real ? lds_ld(&cons[w + 1]) : (1 << 30);
+                        if ((pin > c && pout >= c - R + 1) || lds_ld(&sh_abort)) break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    if (lds_ld(&sh_abort)) break;
+                    t03 = *reinterpret_cast<const int4*>(&tin[slot]);
+                    t47 = *reinterpret_cast<const int4*>(&tin[slot + 4]);
+                }
+                const int T[CH] = {t03.x, t03.y, t03.z, t03.w, t47.x, t47.y, t47.z, t47.w};
+                const uint64_t ch8c = ch8;
+                if (lane == 0) __hip_atomic_store(&cons[w], c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (c + 1 < NC) {
+                    const int nslot = ((c + 1) % R) * CH;
+                    ch8 = *(cptr64)(a.s1 + 8 * (int64_t)(c + 1));
+                    pin = lds_ld(&prog[w]);
+                    t03 = *reinterpret_cast<const int4*>(&tin[nslot]);
+                    t47 = *reinterpret_cast<const int4*>(&tin[nslot + 4]);
+                    if (next_real) pout = lds_ld(&cons[w + 1]);
+                }
+                int* bot_wr = (lane == 63) ? &tring[(w + 1) * R * CH + slot] : &scratch[lane];
+                const int nstep = (c == NC - 1) ? nlast : CH;
+                uint32_t dw;
+                if (c == NC - 1)
+                    chunk_body<SH, SD, ST, true>(a, st, T, ch8c, c, nstep, lane, tile_off, j0, d, vcm, vck, bot_wr, &dw);
+                else
+                    chunk_body<SH, SD, ST, false>(a, st, T, ch8c, c, CH, lane, tile_off, j0, d, vcm, vck, bot_wr, &dw);
+                if (next_real && lane == 0) lds_publish(&prog[w + 1], c + 1);
+                if (jrow > a.L2) dw = 0;
+                if (SD) a.D[((int64_t)g * NC + c) * 64 + lane] = dw;
+                if (ST) st.bc += branch_nibbles(dw);
+                // Last wave of a non-final WG-stripe publishes its bottom row.
+                if (publish) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (lane < nstep) {
+                        const int v = tring[W * R * CH + slot + lane] - 64 * W * d;  // row-above domain
+                        const uint64_t gr = ((uint64_t)(uint32_t)(sidx + 1) << 32) | (uint32_t)v;
+                        __hip_atomic_store(gout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    }
                 }
             }
         }
+        if (a.trace && threadIdx.x == 64 * (W - 1)) a.trace[4 * (int64_t)sidx + 2] = __builtin_amdgcn_s_memrealtime();
         if (ST && real) {
             const bool rowok = jrow <= a.L2;
             int gv = rowok ? st.gav : 0;
@@ -315,36 +451,28 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
     }
 }
 
-// Boundary row/column seeding (computation.c:93-120): row 0, H[i][0] = -i*d,
-// into row0[]; column 0, H[0][j] = -j*d, into slot i = 0 of every stripe.
-// Directions of boundary cells are implicit (code_at).
-__global__ void nw_seed_kernel(int32_t* row0, int32_t* tiles, int64_t spitch, int32_t L1, int32_t NG, int32_t d) {
-    const int64_t n = (int64_t)L1 + 1 + 64 * (int64_t)NG;
-    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n;
-         x += (int64_t)gridDim.x * blockDim.x) {
-        if (x <= L1) row0[x] = (int32_t)(-x * (int64_t)d);
-        else {
-            const int64_t r = x - L1 - 1;          // = j - 1
-            tiles[(r >> 6) * spitch + (r & 63)] = (int32_t)(-(r + 1) * (int64_t)d);
-        }
-    }
-}
-
-__device__ __forceinline__ int32_t score_at(const int32_t* row0, const int32_t* tiles, int64_t spitch, int64_t i,
-                                            int64_t j) {
-    if (j == 0) return row0[i];
-    const int64_t r = j - 1;
-    return tiles[(r >> 6) * spitch + i * 64 + (r & 63)];
+// Score of cell (i, j) in the device layout.  Row 0 and column 0 are the
+// reference's seeds (computation.c:93-120), computed, not stored.  Interior
+// cells live in stripe-major quad tiles: stripe g = (j-1)/64, lane l =
+// (j-1)%64, column quad q = (i-1)/4, r = (i-1)%4 at
+//     g*spitch + (q*64 + l)*4 + r,   spitch = 512*NC,
+// i.e. each lane's 4 consecutive columns are one 16-byte word and one quad of
+// one stripe is 1 KB contiguous.
+__device__ __forceinline__ int32_t score_at(const int32_t* tiles, int64_t spitch, int32_t d, int64_t i, int64_t j) {
+    if (i == 0) return (int32_t)(-j * (int64_t)d);
+    if (j == 0) return (int32_t)(-i * (int64_t)d);
+    const int64_t r = j - 1, c = i - 1;
+    return tiles[(r >> 6) * spitch + (((c >> 2) * 64 + (r & 63)) << 2) + (c & 3)];
 }
 
 // Dense i-major copy of columns [i0, i1): out[(i-i0)*(L2+1) + j].
-__global__ void nw_gather_scores_kernel(const int32_t* row0, const int32_t* tiles, int64_t spitch, int32_t L2,
-                                        int64_t i0, int64_t i1, int32_t* out) {
+__global__ void nw_gather_scores_kernel(const int32_t* tiles, int64_t spitch, int32_t d, int32_t L2, int64_t i0,
+                                        int64_t i1, int32_t* out) {
     const int64_t N = (int64_t)L2 + 1;
     const int64_t n = (i1 - i0) * N;
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n;
          x += (int64_t)gridDim.x * blockDim.x)
-        out[x] = score_at(row0, tiles, spitch, i0 + x / N, x % N);
+        out[x] = score_at(tiles, spitch, d, i0 + x / N, x % N);
 }
 
 __device__ __forceinline__ uint32_t code_at(const uint32_t* D, int32_t NC, int64_t i, int64_t j) {
@@ -378,7 +506,7 @@ __global__ void nw_codes_kernel(const uint32_t* D, int32_t NC, int32_t L2, int64
 }
 
 // Per-column FNV-1a-64 of scores (int32 LE bytes) and codes (1 byte/cell).
-__global__ void nw_colhash_kernel(const int32_t* row0, const int32_t* tiles, int64_t spitch, const uint32_t* D,
+__global__ void nw_colhash_kernel(const int32_t* tiles, int64_t spitch, int32_t d, const uint32_t* D,
                                   int32_t NC, int32_t L1,
                                   int32_t L2, uint64_t* hcol, uint64_t* dcol) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -386,7 +514,7 @@ __global__ void nw_colhash_kernel(const int32_t* row0, const int32_t* tiles, int
     const uint64_t P = 0x100000001b3ULL;
     uint64_t h = 0xcbf29ce484222325ULL, e = 0xcbf29ce484222325ULL;
     for (int64_t j = 0; j <= L2; ++j) {
-        const uint32_t v = (uint32_t)score_at(row0, tiles, spitch, i, j);
+        const uint32_t v = (uint32_t)score_at(tiles, spitch, d, i, j);
         h = (h ^ (v & 0xff)) * P;
         h = (h ^ ((v >> 8) & 0xff)) * P;
         h = (h ^ ((v >> 16) & 0xff)) * P;
@@ -467,13 +595,14 @@ struct nw_table {
     // device buffers
     uint8_t* s1 = nullptr;
     uint8_t* s2 = nullptr;
-    int32_t* H = nullptr;       // score tiles
-    int32_t* row0 = nullptr;    // H[i][0]
+    int32_t* H = nullptr;       // score tiles (score_at)
     uint32_t* D = nullptr;
     int32_t* lastcol = nullptr;
     uint64_t* gran = nullptr;
     size_t gran_bytes = 0;
     uint32_t* ctl = nullptr;
+    uint64_t* trace = nullptr;      // $NW_TRACE: in-kernel timeline
+    int64_t trace_n = 0;
     // results of the last fill
     bool filled = false;
     uint32_t last_mask = 0;
@@ -508,11 +637,11 @@ void nw_table_destroy(nw_table* t) {
     (void)hipFree(t->s1);
     (void)hipFree(t->s2);
     (void)hipFree(t->H);
-    (void)hipFree(t->row0);
     (void)hipFree(t->D);
     (void)hipFree(t->lastcol);
     (void)hipFree(t->gran);
     (void)hipFree(t->ctl);
+    (void)hipFree(t->trace);
     for (auto& e : t->ev)
         if (e) (void)hipEventDestroy(e);
     if (t->stream) (void)hipStreamDestroy(t->stream);
@@ -564,8 +693,8 @@ int nw_table_create(int device, int64_t max_L1, int64_t max_L2, uint32_t out_mas
     if ((rc = alloc((void**)&t->s1, (size_t)(CH * NC + 64)))) return bail(rc);
     if ((rc = alloc((void**)&t->s2, (size_t)(64 * NG + 1024)))) return bail(rc);
     if (out_mask & NW_OUT_SCORES) {
-        if ((rc = alloc((void**)&t->H, (size_t)std::max<int64_t>(NG, 1) * (size_t)(max_L1 + 1) * 256))) return bail(rc);
-        if ((rc = alloc((void**)&t->row0, (size_t)(max_L1 + 1) * 4))) return bail(rc);
+        if ((rc = alloc((void**)&t->H, (size_t)std::max<int64_t>(NG, 1) * (size_t)std::max<int64_t>(NC, 1) * 2048)))
+            return bail(rc);
     }
     if (out_mask & NW_OUT_DIRS) {
         if ((rc = alloc((void**)&t->D, (size_t)std::max<int64_t>(NG, 1) * std::max<int64_t>(NC, 1) * 256))) return bail(rc);
@@ -589,7 +718,7 @@ int nw_table_set_sequences(nw_table* t, const char* s1, int64_t L1, const char* 
     t->L2 = L2;
     t->NC = (L1 + CH - 1) / CH;
     t->NG = (L2 + 63) / 64;
-    t->spitch = 64 * (L1 + 1);
+    t->spitch = 512 * t->NC;
     t->filled = false;
     const size_t n1 = (size_t)(CH * t->NC + 64), n2 = (size_t)(64 * t->NG + 1024);
     HIPCHK(hipMemsetAsync(t->s1, 0, n1, t->stream));
@@ -618,7 +747,6 @@ int nw_table_fill(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mas
     const int64_t L1 = t->L1, L2 = t->L2;
     HIPCHK(hipEventRecord(t->ev[0], t->stream));
     HIPCHK(hipMemsetAsync(t->ctl, 0, CTL_WORDS * 4, t->stream));
-    if (sh) nw_seed_kernel<<<256, 256, 0, t->stream>>>(t->row0, t->H, t->spitch, (int32_t)L1, (int32_t)t->NG, d);
     HIPCHK(hipGetLastError());
     int W = 0;
     if (L1 > 0 && L2 > 0) {
@@ -643,6 +771,18 @@ int nw_table_fill(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mas
         a.gran = t->gran;
         a.gpitch = CH * t->NC + CH;
         a.ctl = t->ctl;
+        if (getenv("NW_TRACE")) {
+            const int64_t need = 4 * (int64_t)a.NSW;
+            if (t->trace_n < need) {
+                (void)hipFree(t->trace);
+                t->trace = nullptr;
+                t->trace_n = 0;
+                HIPCHK(hipMalloc(&t->trace, (size_t)need * 8));
+                t->trace_n = need;
+            }
+            HIPCHK(hipMemsetAsync(t->trace, 0, (size_t)need * 8, t->stream));
+            a.trace = t->trace;
+        }
         int occ = 1;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(fn), 64 * (W + 1), 0));
         occ = std::max(occ, 1);
@@ -666,8 +806,9 @@ int nw_table_fill(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mas
     HIPCHK(hipMemcpyAsync(ctl, t->ctl, sizeof ctl, hipMemcpyDeviceToHost, t->stream));
     int32_t corner = 0;
     if (L1 > 0 && L2 > 0) {
-        const int64_t r = L2 - 1;
-        const int32_t* src = sh ? t->H + (r >> 6) * t->spitch + L1 * 64 + (r & 63) : t->lastcol + L2;
+        const int64_t r = L2 - 1, q = L1 - 1;
+        const int32_t* src = sh ? t->H + (r >> 6) * t->spitch + (((q >> 2) * 64 + (r & 63)) << 2) + (q & 3)
+                                : t->lastcol + L2;
         HIPCHK(hipMemcpyAsync(&corner, src, 4, hipMemcpyDeviceToHost, t->stream));
     }
     HIPCHK(hipStreamSynchronize(t->stream));
@@ -703,6 +844,15 @@ int nw_table_elapsed_ms(nw_table* t, float* kernel_ms, float* call_ms) {
     return NW_OK;
 }
 
+int64_t nw_table_trace(nw_table* t, uint64_t* dst, int64_t n) {
+    if (!t || !t->trace) return 0;
+    const int64_t m = std::min(n, t->trace_n);
+    if (m > 0 && dst) {
+        if (hipMemcpy(dst, t->trace, (size_t)m * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    }
+    return t->trace_n;
+}
+
 int64_t nw_table_score_pitch(const nw_table* t) { return t ? t->spitch : 0; }
 int nw_table_waves(const nw_table* t) { return t ? t->waves : 0; }
 
@@ -715,7 +865,7 @@ static int copy_scores_impl(nw_table* t, int64_t i0, int64_t i1, int32_t* dst) {
     hipError_t e = hipSuccess;
     for (int64_t c0 = i0; c0 < i1 && e == hipSuccess; c0 += cols_per) {
         const int64_t c1 = std::min(i1, c0 + cols_per);
-        nw_gather_scores_kernel<<<1024, 256, 0, t->stream>>>(t->row0, t->H, t->spitch, (int32_t)t->L2, c0, c1, stage);
+        nw_gather_scores_kernel<<<1024, 256, 0, t->stream>>>(t->H, t->spitch, t->last_d, (int32_t)t->L2, c0, c1, stage);
         e = hipGetLastError();
         if (e == hipSuccess)
             e = hipMemcpyAsync(dst + (c0 - i0) * N, stage, (size_t)((c1 - c0) * N * 4), hipMemcpyDeviceToHost, t->stream);
@@ -777,7 +927,8 @@ int nw_table_hash(nw_table* t, uint64_t* hH, uint64_t* hD) {
     HIPCHK(hipMalloc(&dh, (size_t)ncol * 16));
     const bool have_d = (t->last_mask & NW_OUT_DIRS) != 0;
     nw_colhash_kernel<<<(unsigned)((ncol + 255) / 256), 256, 0, t->stream>>>(
-        t->row0, t->H, t->spitch, have_d ? t->D : nullptr, (int32_t)t->NC, (int32_t)t->L1, (int32_t)t->L2, dh, dh + ncol);
+        t->H, t->spitch, t->last_d, have_d ? t->D : nullptr, (int32_t)t->NC, (int32_t)t->L1, (int32_t)t->L2, dh,
+        dh + ncol);
     std::vector<uint64_t> hv((size_t)ncol * 2);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(hv.data(), dh, (size_t)ncol * 16, hipMemcpyDeviceToHost, t->stream);

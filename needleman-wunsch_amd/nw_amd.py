@@ -45,6 +45,7 @@ EXPORTS = (
     "nw_table_create", "nw_table_destroy", "nw_table_set_sequences", "nw_table_fill",
     "nw_table_stats", "nw_table_elapsed_ms", "nw_table_hash", "nw_table_copy_scores",
     "nw_table_copy_codes", "nw_table_copy_last_column", "nw_table_score_pitch", "nw_table_waves",
+    "nw_table_trace",
 )
 
 
@@ -107,6 +108,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.nw_table_copy_last_column.argtypes = [c_p, c_p]
     lib.nw_table_score_pitch.restype = c_i64
     lib.nw_table_score_pitch.argtypes = [c_p]
+    lib.nw_table_trace.restype = c_i64
+    lib.nw_table_trace.argtypes = [c_p, c_p, c_i64]
     lib.nw_table_waves.restype = ctypes.c_int
     lib.nw_table_waves.argtypes = [c_p]
     _lib = lib
@@ -223,6 +226,14 @@ class Table:
         out = np.empty(self.L2 + 1, dtype=np.int32)
         _check(self._lib.nw_table_copy_last_column(self._h, out.ctypes.data), "nw_table_copy_last_column")
         return out
+
+    def trace(self) -> np.ndarray:
+        """In-kernel timeline (needs $NW_TRACE): rows (dequeue, start, end, block|cu<<32)."""
+        n = self._lib.nw_table_trace(self._h, None, 0)
+        out = np.zeros(max(n, 0), dtype=np.uint64)
+        if n > 0:
+            self._lib.nw_table_trace(self._h, out.ctypes.data, n)
+        return out.reshape(-1, 4)
 
     @property
     def waves(self) -> int:
