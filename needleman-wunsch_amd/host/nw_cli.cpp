@@ -1,0 +1,140 @@
+// nw_cli.cpp -- `needleman-wunsch`, the reference CLI over the GPU fill.
+//
+// Same options, operands, messages and exit codes as the reference driver
+// (needleman-wunsch.c:65-89 usage, :698-795 main, dbg.c:7-15 program name,
+// dbg.h:67-100 error format).  Between reading the sequences and printing,
+// compute_table_scores() (needleman-wunsch.c:583) is replaced by nw_fill()
+// (include/nw_fill.h) on the GPU.  -p N is accepted and validated exactly as
+// in the reference (it must be > 1) but the fill always runs on the GPU:
+// there is no CPU path.  Failure to run the GPU fill is an error (exit 1).
+#include <getopt.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "nw_fill.h"
+#include "nw_host.h"
+
+namespace {
+
+const char* g_prog = "needleman-wunsch";
+
+void log_err_errno(const char* msg) {
+    fprintf(stderr, "%s: error: %s: %s\n", g_prog, msg, errno == 0 ? "\b\b \b" : strerror(errno));
+}
+
+[[noreturn]] void usage() {
+    fputs("usage: needleman-wunsch [-c][-h][-l][-q][-s][-t][-u]\n"
+          "                        [-p num-threads] [-f sequence-file] m k d\n"
+          "Align two sequences with the Needleman-Wunsch algorithm\n"
+          "operands:\n"
+          "   m   match bonus\n"
+          "   k   mismatch penalty\n"
+          "   d   indel (gap) penalty\n"
+          "options:\n"
+          "  -c   color the output with ANSI escape sequences\n"
+          "  -f sequence-file\n"
+          "       read the input strings from 'sequence-file' instead of standard input\n"
+          "  -h   print this usage message\n"
+          "  -l   list match, mismatch, and indel counts for each alignment pair\n"
+          "  -p num-threads\n"
+          "       parallelize the computation with 'num-threads' threads (must be >1)\n"
+          "  -q   be quiet and don't print the aligned strings\n"
+          "  -s   summarize the algorithm's run\n"
+          "  -t   print the scores table; only useful for shorter input strings\n"
+          "  -u   use unicode arrows when printing the scores table\n",
+          stderr);
+    exit(1);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argv[0][0] == '.' && argv[0][1] == '/') g_prog = argv[0] + 2;
+    else g_prog = argv[0];
+    errno = 0;
+
+    nwh_flags f{};
+    const char* infile = nullptr;
+    int c;
+    char msg[256];
+    while ((c = getopt(argc, argv, "cf:hlp:qstu")) != -1) {
+        switch (c) {
+            case 'c': f.cflag = 1; break;
+            case 'f': infile = optarg; break;
+            case 'h': usage();
+            case 'l': f.lflag = 1; break;
+            case 'p': {
+                const int nthreads = atoi(optarg);
+                if (!(nthreads > 1)) {
+                    snprintf(msg, sizeof msg, "num-threads == %d; num-threads must be greater than 1", nthreads);
+                    log_err_errno(msg);
+                    exit(1);
+                }
+                break;
+            }
+            case 'q': f.qflag = 1; break;
+            case 's': f.sflag = 1; break;
+            case 't': f.tflag = 1; break;
+            case 'u': f.uflag = 1; break;
+            default: usage();
+        }
+    }
+    const int nops = argc - optind;
+    if (nops != 3) {
+        snprintf(msg, sizeof msg, "expected %d operands but received%s %d", 3,
+                 (nops > 3 || nops == 0) ? "" : " only", nops);
+        log_err_errno(msg);
+        usage();
+    }
+    FILE* in = stdin;
+    if (infile) {
+        in = fopen(infile, "r");
+        if (!in) {
+            snprintf(msg, sizeof msg, "failed to open %s", infile);
+            log_err_errno(msg);
+            exit(1);
+        }
+    }
+    char *s1 = nullptr, *s2 = nullptr;
+    if (nwh_read_two_sequences(in, g_prog, &s1, &s2) != 0) exit(1);
+    const int m = atoi(argv[optind + 0]);
+    const int k = atoi(argv[optind + 1]);
+    const int d = atoi(argv[optind + 2]);
+
+    // ---- the fill (GPU) -----------------------------------------------------
+    const int64_t L1 = (int64_t)strlen(s1), L2 = (int64_t)strlen(s2);
+    const int64_t ncell = (L1 + 1) * (L2 + 1);
+    const bool want_codes = nwh_needs_traceback(&f) || f.tflag;
+    std::vector<int32_t> H;
+    std::vector<uint8_t> nib, codes;
+    if (f.tflag) H.resize((size_t)ncell);
+    if (want_codes) nib.resize((size_t)((ncell + 1) / 2));
+    nw_stats st{};
+    const int rc = nw_fill(s1, L1, s2, L2, m, k, d, f.tflag ? (uint32_t)NW_OUT_STATS : 0u, -1, f.tflag ? H.data() : nullptr,
+                           want_codes ? nib.data() : nullptr, &st);
+    if (rc != NW_OK) {
+        fprintf(stderr, "%s: error: GPU fill failed: %s: %s\n", g_prog, nw_strerror(rc), nw_last_error());
+        exit(1);
+    }
+    if (want_codes) {
+        codes.resize((size_t)ncell);
+        for (int64_t x = 0; x < ncell; ++x) codes[(size_t)x] = (uint8_t)((nib[(size_t)(x >> 1)] >> (4 * (x & 1))) & 0xf);
+        std::vector<uint8_t>().swap(nib);
+    }
+    if (nwh_render(s1, s2, &f, f.tflag ? H.data() : nullptr, want_codes ? codes.data() : nullptr, st.corner,
+                   st.greatest_abs_interior, stdout, stderr) != 0) {
+        errno = ENOMEM;
+        log_err_errno("malloc failed");
+        exit(1);
+    }
+    free(s1);
+    free(s2);
+    if (in != stdin) fclose(in);
+    return 0;
+}

@@ -1,0 +1,128 @@
+"""Host side of the CLI on CPU (no GPU): argument/reader error paths of the
+real binary, and the traceback/summary/table renderer (libnwhost.so) fed with
+oracle tables, both byte-compared with the reference's own output
+(tests/golden/cli_cases.json, produced by oracle/_ref/needleman-wunsch)."""
+import ctypes
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from conftest import ROOT, load_golden
+
+PKG = os.path.join(ROOT, "needleman-wunsch_amd")
+CLI = os.path.join(PKG, "bin", "needleman-wunsch")
+HOSTLIB = os.path.join(PKG, "lib", "libnwhost.so")
+CASES = load_golden("cli_cases.json")
+
+
+def _built():
+    if not (os.path.exists(CLI) and os.path.exists(HOSTLIB)):
+        subprocess.check_call(["make", "-s", "-C", PKG, "cli", "hostlib"])
+
+
+def run_cli(case):
+    """Run the CLI as `needleman-wunsch` (argv[0] matters, dbg.c:7-15)."""
+    _built()
+    args, stdin, tmp = list(case["args"]), case["stdin"], None
+    if "{FILE}" in args:
+        tmp = tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False)
+        tmp.write(stdin)
+        tmp.close()
+        args = [tmp.name if a == "{FILE}" else a for a in args]
+        stdin = ""
+    try:
+        p = subprocess.run(["needleman-wunsch"] + args, executable=CLI, input=stdin.encode(),
+                           capture_output=True, timeout=300)
+    finally:
+        if tmp:
+            os.unlink(tmp.name)
+    return p.returncode, p.stdout.decode("utf-8", "replace"), p.stderr.decode("utf-8", "replace")
+
+
+class Flags(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("cflag", "lflag", "qflag", "sflag", "tflag", "uflag")]
+
+
+def parse_args(args):
+    """getopt "cf:hlp:qstu" for the success cases of the golden set."""
+    f, ops, i = Flags(), [], 0
+    while i < len(args):
+        a = args[i]
+        if a == "--":
+            ops += args[i + 1:]
+            break
+        if a.startswith("-") and len(a) > 1 and not ops:
+            for ch in a[1:]:
+                if ch in "cqlstu":
+                    setattr(f, ch + "flag", 1)
+                elif ch in "fp":
+                    i += 1
+                    break
+            i += 1
+            continue
+        ops.append(a)
+        i += 1
+    return f, [int(x) for x in ops]
+
+
+def read_two(text):
+    """read-sequences.c:43-122 semantics for the success cases."""
+    b = text.encode()
+    ws = b" \t\n\v\f\r"
+    i = 0
+    while i < len(b) and b[i] not in ws:
+        i += 1
+    s1 = b[:i]
+    i += 1
+    while i < len(b) and b[i] in ws:
+        i += 1
+    j = i
+    while j < len(b) and b[j] not in ws:
+        j += 1
+    return s1, b[i:j]
+
+
+def render(case):
+    lib = ctypes.CDLL(HOSTLIB)
+    f, (m, k, d) = parse_args(case["args"])
+    s1, s2 = read_two(case["stdin"])
+    H, D, (corner, gav, bc) = O.fill(s1, s2, m, k, d)
+    out, err = ctypes.c_char_p(), ctypes.c_char_p()
+    on, en = ctypes.c_size_t(), ctypes.c_size_t()
+    lib.nwh_render_to_buffers.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Flags),
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                          ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t)]
+    H = np.ascontiguousarray(H)
+    D = np.ascontiguousarray(D)
+    rc = lib.nwh_render_to_buffers(s1, s2, ctypes.byref(f), H.ctypes.data, D.ctypes.data, corner, gav,
+                                   ctypes.byref(out), ctypes.byref(on), ctypes.byref(err), ctypes.byref(en))
+    assert rc == 0
+    o = ctypes.string_at(out, on.value).decode("utf-8")
+    e = ctypes.string_at(err, en.value).decode("utf-8")
+    return o, e
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["rc"] != 0], ids=lambda c: c["name"])
+def test_cli_error_paths_match_reference(case):
+    assert run_cli(case) == (case["rc"], case["stdout"], case["stderr"])
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["rc"] == 0], ids=lambda c: c["name"])
+def test_renderer_matches_reference(case):
+    _built()
+    o, e = render(case)
+    assert o == case["stdout"]
+    assert e == case["stderr"]
+
+
+def test_golden_set_covers_readme_examples():
+    names = {c["name"] for c in CASES}
+    for n in ("readme_table_q_s_t", "gat_gta", "gat_gta_s", "gat_gta_l", "gt_gt", "gt_ga"):
+        assert n in names
+    readme = next(c for c in CASES if c["name"] == "readme_table_q_s_t")
+    assert readme["stderr"] == "3 optimal alignments\nOptimal score is 0\n"

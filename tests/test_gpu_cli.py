@@ -1,0 +1,35 @@
+"""End-to-end CLI on the GPU: every golden case of the reference CLI
+(tests/golden/cli_cases.json) must be reproduced byte for byte (stdout,
+stderr, exit status) by needleman-wunsch_amd/bin/needleman-wunsch, whose fill
+runs through libnwfill.so on the MI355X."""
+import pytest
+
+from conftest import load_golden
+from test_cli_host import run_cli
+
+pytestmark = pytest.mark.gpu
+CASES = load_golden("cli_cases.json")
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c["name"])
+def test_cli_matches_reference(case):
+    assert run_cli(case) == (case["rc"], case["stdout"], case["stderr"])
+
+
+def test_cli_large_summary_and_quiet():
+    """CLI on longer inputs.  -q alone skips the traceback (needleman-wunsch.c:667);
+    -s runs it, so use a near-identical pair whose optimum is a single alignment
+    (random pairs have exponentially many co-optimal alignments -- the
+    reference's enumeration would not finish either, README:195-200)."""
+    import oracle_lib as O
+    s1 = bytearray(O.gen_dna(41, 3000))
+    s2 = bytearray(s1)
+    for p in (17, 1234, 2999):
+        s2[p] = ord("A") if s2[p] != ord("A") else ord("C")
+    s1, s2 = bytes(s1), bytes(s2)
+    H, D, st = O.fill(s1, s2, 1, 1, 1)
+    rc, out, err = run_cli({"args": ["-q", "1", "1", "1"], "stdin": (s1 + b" " + s2 + b"\n").decode()})
+    assert (rc, out, err) == (0, "", "")
+    rc, out, err = run_cli({"args": ["-q", "-s", "1", "1", "1"], "stdin": (s1 + b" " + s2 + b"\n").decode()})
+    assert rc == 0 and out == ""
+    assert err == f"1 optimal alignment\nOptimal score is {st[0]}\n"
