@@ -9,7 +9,8 @@ resident in HBM.  value = L1*L2 / (ms_per_step) in GCUPS (whole job).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   N > 1: launched by torch.distributed.run, one rank per GPU; the table is
-         split into column panels across ranks (strong scaling).
+         split into row panels across ranks (strong scaling, bench_multi.py,
+         DESIGN.md "Multi-GPU").
 
 Extra JSON fields:
   roofline     -- fill kernel's algorithmic bytes (4.5 B/cell: 4 B score +
@@ -49,6 +50,13 @@ def parse():
                          "('' = score-only); the metric's workload is 'sd'")
     ap.add_argument("--cpu-sample", type=int, default=14142,
                     help="side of the square sample the CPU reference fills (~2e8 cells)")
+    ap.add_argument("--transport", choices=("ipc", "rccl"), default="ipc",
+                    help="N > 1: how a panel's bottom row reaches the next GPU (bench_multi.py)")
+    ap.add_argument("--pg-backend", default="nccl",
+                    help="N > 1: torch.distributed backend for barriers (gloo only to rehearse "
+                         "several ranks on one GPU)")
+    ap.add_argument("--device", type=int, default=None,
+                    help="N > 1: force every rank onto this device (rehearsal on one GPU)")
     return ap.parse_args()
 
 
@@ -116,7 +124,7 @@ def run_single(a):
 def main():
     a = parse()
     if a.gpus != 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        import bench_multi  # column-panel strong scaling over RCCL (N > 1)
+        import bench_multi  # row-panel strong scaling (N > 1)
         return bench_multi.main(a)
     L1, L2 = a.L1, a.L2
     dt, kern, waves, corner = run_single(a)

@@ -65,7 +65,8 @@ enum nw_err {
         NW_ERR_HIP       = -4,  /* a HIP runtime call failed                   */
         NW_ERR_RANGE     = -5,  /* int32 overflow possible for these inputs    */
         NW_ERR_TIMEOUT   = -6,  /* in-kernel hand-off watchdog fired           */
-        NW_ERR_STATE     = -7   /* call out of order (e.g. no sequences set)   */
+        NW_ERR_STATE     = -7,  /* call out of order (e.g. no sequences set)   */
+        NW_ERR_PEER      = -8   /* a peer panel failed (nw_panel.h)            */
 };
 
 const char *nw_strerror(int rc);

@@ -1,0 +1,116 @@
+/* nw_panel.h -- multi-GPU row panels for the MI355X score-table fill.
+ *
+ * The reference fills one table in one process; its only parallelism is the
+ * pthread column-cyclic schedule of `-p` (needleman-wunsch.c:444-475,
+ * :557-574, :583-626), where thread t owns columns t+1, t+1+T, ... and waits
+ * per cell for its left neighbour.  Across GPUs the table is split instead into
+ * contiguous ROW panels: panel r holds global rows row_base+1 .. row_base+rows
+ * (whole 64-row stripes; every panel but the last has a multiple of 64 rows)
+ * for all columns.  This is SURVEY.md section 8(e)'s column-panel scheme
+ * transposed to this fill's stripe orientation (waves sweep columns): the
+ * exchange is the single boundary ROW, in blocks of columns, and a panel
+ * starts as soon as the first block of the row above it is done.
+ *
+ * Each panel's kernel publishes its bottom row as tagged 8-byte granules
+ * {epoch, H - d}; the panel below polls the tags, so no barrier or host
+ * round trip sits between producer and consumer.  Two transports move the
+ * granules (enum nw_panel_transport):
+ *   - GROUP / IPC: the producer's kernel stores straight into the consumer's
+ *     boundary buffer (same GPU, or a peer GPU over xGMI; across processes
+ *     the buffer is mapped with hipIpcOpenMemHandle), no host involvement.
+ *   - RCCL: a host proxy waits for the producer's per-block flag (pinned host
+ *     memory) and issues ncclSend; the consumer posts its ncclRecvs up front.
+ *     Two communicators, so a rank's send and receive links never share one.
+ * A failed panel poisons the row it owes (tag = epoch | 2^31) so the panels
+ * below stop with NW_ERR_PEER instead of waiting for the watchdog.
+ *
+ * Stats of the whole table are bit-identical to a single-GPU fill: corner
+ * from the last panel, max of greatest_abs_interior, sum of branch_count.  The local rows stay device-resident in the panel's
+ * nw_table (nw_panel_table), local row j = global row row_base + j; its row
+ * 0 is the last row of the panel above (scores exact, codes read as 0).
+ */
+#ifndef NW_PANEL_H
+#define NW_PANEL_H
+
+#include <stdint.h>
+
+#include "nw_fill.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct nw_panel nw_panel;
+
+/* How a panel's bottom row reaches the panel below. */
+enum nw_panel_transport {
+        NW_PANEL_GROUP = 0,  /* one process, n panels: direct device stores        */
+        NW_PANEL_IPC   = 1,  /* one process per GPU: direct stores into the peer's  */
+                             /* boundary buffer, mapped with hipIpc (xGMI)          */
+        NW_PANEL_RCCL  = 2   /* one process per GPU: host proxy + ncclSend/ncclRecv */
+};
+
+#define NW_PANEL_ID_BYTES  256  /* RCCL rendezvous: two ncclUniqueId           */
+#define NW_PANEL_IPC_BYTES 64   /* hipIpcMemHandle_t of a boundary buffer      */
+#define NW_PANEL_REC       8    /* int64 words of one rank's stats record      */
+
+/* Row split of an L2-row table over nranks panels: whole 64-row stripes,
+ * balanced to within one stripe.  Pure host logic (no device needed). */
+int nw_panel_partition(int64_t L2, int nranks, int rank, int64_t *row_base, int64_t *rows);
+
+/* Panels that exchange boundary rows (empty panels are skipped): the rank
+ * above (*prev) and below (*next) `rank`, -1 when none, and its position in
+ * that chain (-1 for an empty panel).  Pure host logic. */
+int nw_panel_chain(int64_t L2, int nranks, int rank, int *prev, int *next, int *pos);
+
+/* RCCL only, rank 0: create the rendezvous id; the caller broadcasts it. */
+int nw_panel_get_id(uint8_t id[NW_PANEL_ID_BYTES]);
+
+/* One process per GPU (transport IPC or RCCL).  For RCCL this is collective
+ * over the nranks processes and `id` is rank 0's nw_panel_get_id(); for IPC
+ * `id` is ignored and the ranks then swap nw_panel_ipc_handle()s and call
+ * nw_panel_ipc_connect().  max_L2 is the GLOBAL row capacity. */
+int nw_panel_create(int transport, int device, int rank, int nranks, const uint8_t *id,
+                    int64_t max_L1, int64_t max_L2, uint32_t out_mask, nw_panel **out);
+int nw_panel_ipc_handle(nw_panel *p, uint8_t handle[NW_PANEL_IPC_BYTES]);
+/* handles: every rank's handle, in rank order (nranks * NW_PANEL_IPC_BYTES). */
+int nw_panel_ipc_connect(nw_panel *p, const uint8_t *handles);
+
+/* In-process group of n panels on devices[0..n-1] (repeats allowed, e.g. n
+ * panels on one GPU; distinct GPUs get peer access).  out[0..n-1]. */
+int nw_panel_group_create(int n, const int *devices, int64_t max_L1, int64_t max_L2, uint32_t out_mask,
+                          nw_panel **out);
+
+void nw_panel_destroy(nw_panel *p);   /* group panels: destroy each one */
+
+/* Full sequences (same on every rank); the panel uploads its own rows. */
+int nw_panel_set_sequences(nw_panel *p, const char *s1, int64_t L1, const char *s2, int64_t L2);
+
+/* IPC / RCCL: every rank calls it once per fill, same arguments.  Returns
+ * this rank's status; a failure upstream surfaces as NW_ERR_PEER. */
+int nw_panel_fill(nw_panel *p, int32_t m, int32_t k, int32_t d, uint32_t out_mask);
+
+/* In-process group: fills all n panels of the group, in rank order. */
+int nw_panel_group_fill(nw_panel *const *ps, int n, int32_t m, int32_t k, int32_t d, uint32_t out_mask);
+
+/* Whole-table stats.  A group computes them itself (nw_panel_stats on any of
+ * its panels).  Across processes the caller gathers every rank's record
+ * (nw_panel_record, after the fill) and reduces them with nw_panel_reduce --
+ * a few words of control traffic, left to the caller's own collective. */
+int nw_panel_stats(nw_panel *p, nw_stats *st);
+int nw_panel_record(nw_panel *p, int64_t rec[NW_PANEL_REC]);
+int nw_panel_reduce(const int64_t *recs, int nranks, nw_stats *st);   /* pure; first error wins */
+
+/* This panel's rows and its device-resident table (owned by the panel). */
+int nw_panel_rows(const nw_panel *p, int64_t *row_base, int64_t *rows);
+nw_table *nw_panel_table(nw_panel *p);
+
+/* Milliseconds of the last fill: this panel's kernel (HIP events) and the
+ * whole nw_panel_fill call on the host clock. */
+int nw_panel_elapsed_ms(nw_panel *p, float *kernel_ms, float *call_ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NW_PANEL_H */

@@ -36,12 +36,16 @@
 #include <string>
 #include <vector>
 
-#include "nw_fill.h"
+#include "nw_internal.h"
 
 namespace {
 
 constexpr int CH = 8;                 // columns per chunk (= codes per dirs word)
 constexpr int64_t SPIN_TICKS = 200000000;  // 2 s of s_memrealtime (100 MHz)
+// Panel boundary granule tags: the fill's epoch (1 .. 2^31-1), or the epoch
+// with bit 31 set when the panel above failed that fill (per-epoch, so a stale
+// poison never trips a later fill).
+constexpr uint32_t POISON_BIT = 0x80000000u;
 
 enum CtlWord { CTL_NEXT = 0, CTL_ABORT = 1, CTL_GAV = 2, CTL_BC = 3, CTL_ERR = 4, CTL_WORDS = 16 };
 
@@ -62,6 +66,15 @@ struct FillArgs {
     int32_t nslot;
     uint32_t* ctl;          // CtlWord
     uint64_t* trace;        // optional timeline: 4 words per WG-stripe (see nw_table_trace)
+    int64_t spin_ticks;     // hand-off watchdog (s_memrealtime ticks)
+    // Row panels (multi-GPU, nw_panel.h).  The table holds global rows
+    // row_base+1 .. row_base+L2; row 0 is the boundary row of the panel above.
+    int32_t row_base;
+    uint32_t epoch;         // tag of this fill's panel hand-off granules
+    const uint64_t* xin;    // top boundary row {epoch, H-d} per column, or null (= seeded row 0)
+    uint64_t* xout;         // bottom row granules for the panel below, or null
+    uint32_t* xflag;        // host-visible: xflag[b] = epoch once block b of xout is written
+    int32_t xblk;           // chunks per block
 };
 
 // ---------------------------------------------------------------- DPP helpers
@@ -247,6 +260,13 @@ __device__ __forceinline__ void chunk_body(const FillArgs& a, WaveState& st, con
     *dword_out = acc;
 }
 
+// Hand-off granule load: agent scope between workgroups of one fill, system
+// scope (bypassing L2) for the panel boundary, which another agent writes.
+__device__ __forceinline__ uint64_t ld_gran(const uint64_t* p, bool sys) {
+    return sys ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+               : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // LDS counters of the barrier-free intra-workgroup pipeline.
 __device__ __forceinline__ int lds_ld(const int* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -316,37 +336,43 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
 
         if (loader) {
             // ---------------- loader wave: no stores, exact waits ----------------
-            const uint64_t* gin = a.gran + (int64_t)(sidx % a.nslot) * a.gpitch;
+            // Source of the WG-stripe's top row: the seeded row 0, the panel
+            // above (xin, written by another agent: system-scope loads), or
+            // the previous WG-stripe's granules (agent scope).
+            const bool seeded = sidx == 0 && !a.xin;
+            const bool xsrc = sidx == 0 && a.xin;
+            const uint64_t* gin = xsrc ? a.xin : a.gran + (int64_t)(sidx % a.nslot) * a.gpitch;
+            const uint32_t want = xsrc ? a.epoch : (uint32_t)sidx;
             uint64_t pf = 0;
-            if (sidx > 0 && lane < CH)
-                pf = __hip_atomic_load(gin + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!seeded && lane < CH) pf = ld_gran(gin + lane, xsrc);
             for (int c = 0; c < NC; ++c) {
                 const int n = (c == NC - 1) ? nlast : CH;
                 while (lds_ld(&cons[0]) < c - R + 1) __builtin_amdgcn_s_sleep(1);   // ring slot free?
                 int* dst = &tring[(c % R) * CH];
-                if (sidx == 0) {
+                if (seeded) {
                     // row 0: H[i][0] - d = -(i+1)*d   (computation.c:102-110)
                     if (lane < CH) dst[lane] = -(CH * c + 2 + lane) * d;
                 } else {
-                    const uint32_t want = (uint32_t)sidx;
                     bool ok = lane >= n || (uint32_t)(pf >> 32) == want;
                     if (!__all(ok)) {
                         const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
                         for (;;) {
                             __builtin_amdgcn_s_sleep(1);
-                            if (!ok)
-                                pf = __hip_atomic_load(gin + CH * (int64_t)c + lane, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
+                            if (!ok) pf = ld_gran(gin + CH * (int64_t)c + lane, xsrc);
                             ok = lane >= n || (uint32_t)(pf >> 32) == want;
                             if (__all(ok)) break;
                             const int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
                             const uint32_t ab = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED,
                                                                   __HIP_MEMORY_SCOPE_AGENT);
-                            if (ab || now - t0 > SPIN_TICKS) {
+                            // a failed panel above poisons its boundary row
+                            const bool peer = xsrc && __any(lane < n && (uint32_t)(pf >> 32) == (want | POISON_BIT));
+                            if (ab || peer || now - t0 > a.spin_ticks) {
                                 if (lane == 0) {
                                     __hip_atomic_store(&a.ctl[CTL_ABORT], 1u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT);
-                                    if (!ab) atomicCAS(&a.ctl[CTL_ERR], 0u, (uint32_t)NW_ERR_TIMEOUT);
+                                    if (!ab)
+                                        atomicCAS(&a.ctl[CTL_ERR], 0u,
+                                                  (uint32_t)(peer ? NW_ERR_PEER : NW_ERR_TIMEOUT));
                                     __hip_atomic_store(&sh_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                                 }
                                 break;
@@ -356,8 +382,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
                     if (lds_ld(&sh_abort)) break;
                     if (lane < CH) dst[lane] = (int)(uint32_t)pf;
                     if (c + 1 < NC && lane < CH)          // prefetch the next chunk
-                        pf = __hip_atomic_load(gin + CH * (int64_t)(c + 1) + lane, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
+                        pf = ld_gran(gin + CH * (int64_t)(c + 1) + lane, xsrc);
                 }
                 if (lane == 0) lds_publish(&prog[0], c + 1);
             }
@@ -367,10 +392,13 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             const int64_t tile_off = (int64_t)g * a.spitch;
             st.c2 = a.s2[jrow - 1];
             st.laneoff = (64 * w + lane) * d;
-            // column 0: H[0][j] = -j*d  ->  G = -(1 + 64*sidx*W)*d for every lane.
-            st.G = -(1 + 64 * sidx * W) * d;
+            // column 0: H[0][j] = -j*d  ->  G = -(1 + row_base + 64*sidx*W)*d for every lane.
+            st.G = -(1 + a.row_base + 64 * sidx * W) * d;
             st.Tprev = st.G;
             const bool publish = (w == W - 1) && sidx + 1 < a.NSW;
+            // The wave holding the panel's last row (lane 63: panels above the
+            // last one have a multiple of 64 rows) feeds the panel below.
+            const bool xpublish = a.xout && g == a.NG - 1;
             const int* tin = &tring[w * R * CH];
             if (a.trace && lane == 0 && w == 0) a.trace[4 * (int64_t)sidx + 1] = __builtin_amdgcn_s_memrealtime();
             // Chunk prologue, software-pipelined one chunk ahead: the s1 bytes
@@ -430,6 +458,22 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
                                            __HIP_MEMORY_SCOPE_AGENT);
                     }
                 }
+                if (xpublish) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (lane < nstep) {
+                        const int v = tring[(w + 1) * R * CH + slot + lane] - 64 * (w + 1) * d;
+                        const uint64_t gr = ((uint64_t)a.epoch << 32) | (uint32_t)v;
+                        __hip_atomic_store(a.xout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                    if (a.xflag && ((c + 1) % a.xblk == 0 || c == NC - 1)) {
+                        // block complete: its granules are out before the flag
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (lane == 0)
+                            __hip_atomic_store(&a.xflag[c / a.xblk], a.epoch, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                }
             }
         }
         if (a.trace && threadIdx.x == 64 * (W - 1)) a.trace[4 * (int64_t)sidx + 2] = __builtin_amdgcn_s_memrealtime();
@@ -451,96 +495,100 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
     }
 }
 
+// Mark granules [0, n) of a panel boundary as "the producer failed this fill".
+__global__ void nw_poison_kernel(uint64_t* p, int64_t n, uint32_t epoch) {
+    const uint64_t g = ((uint64_t)(epoch | POISON_BIT) << 32);
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n; x += (int64_t)gridDim.x * blockDim.x)
+        __hip_atomic_store(p + x, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Device view of a filled table for the copy / hash kernels.
+struct TableView {
+    const int32_t* tiles;   // score tiles
+    int64_t spitch;
+    const uint32_t* D;      // codes, or null
+    int32_t NC;
+    int32_t d;
+    int32_t row_base;       // panels: global row of local row 0
+    const uint64_t* top;    // panels: boundary row granules (H - d), or null for row 0 = seed
+};
+
 // Score of cell (i, j) in the device layout.  Row 0 and column 0 are the
-// reference's seeds (computation.c:93-120), computed, not stored.  Interior
-// cells live in stripe-major quad tiles: stripe g = (j-1)/64, lane l =
-// (j-1)%64, column quad q = (i-1)/4, r = (i-1)%4 at
+// reference's seeds (computation.c:93-120), computed, not stored; a panel's
+// row 0 is the last row of the panel above, kept in its xin granules.
+// Interior cells live in stripe-major quad tiles: stripe g = (j-1)/64, lane
+// l = (j-1)%64, column quad q = (i-1)/4, r = (i-1)%4 at
 //     g*spitch + (q*64 + l)*4 + r,   spitch = 512*NC,
 // i.e. each lane's 4 consecutive columns are one 16-byte word and one quad of
 // one stripe is 1 KB contiguous.
-__device__ __forceinline__ int32_t score_at(const int32_t* tiles, int64_t spitch, int32_t d, int64_t i, int64_t j) {
-    if (i == 0) return (int32_t)(-j * (int64_t)d);
-    if (j == 0) return (int32_t)(-i * (int64_t)d);
+__device__ __forceinline__ int32_t score_at(const TableView& v, int64_t i, int64_t j) {
+    if (i == 0) return (int32_t)(-(j + v.row_base) * (int64_t)v.d);
+    if (j == 0) return v.top ? (int32_t)(uint32_t)v.top[i - 1] + v.d : (int32_t)(-i * (int64_t)v.d);
     const int64_t r = j - 1, c = i - 1;
-    return tiles[(r >> 6) * spitch + (((c >> 2) * 64 + (r & 63)) << 2) + (c & 3)];
+    return v.tiles[(r >> 6) * v.spitch + (((c >> 2) * 64 + (r & 63)) << 2) + (c & 3)];
 }
 
 // Dense i-major copy of columns [i0, i1): out[(i-i0)*(L2+1) + j].
-__global__ void nw_gather_scores_kernel(const int32_t* tiles, int64_t spitch, int32_t d, int32_t L2, int64_t i0,
-                                        int64_t i1, int32_t* out) {
+__global__ void nw_gather_scores_kernel(TableView v, int32_t L2, int64_t i0, int64_t i1, int32_t* out) {
     const int64_t N = (int64_t)L2 + 1;
     const int64_t n = (i1 - i0) * N;
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n;
          x += (int64_t)gridDim.x * blockDim.x)
-        out[x] = score_at(tiles, spitch, d, i0 + x / N, x % N);
+        out[x] = score_at(v, i0 + x / N, x % N);
 }
 
-__device__ __forceinline__ uint32_t code_at(const uint32_t* D, int32_t NC, int64_t i, int64_t j) {
+// Direction code of cell (i, j).  A panel's row 0 belongs to the panel above
+// and reads as 0 here.
+__device__ __forceinline__ uint32_t code_at(const TableView& v, int64_t i, int64_t j) {
+    if (j == 0 && v.row_base > 0) return 0u;
     if (i == 0) return j == 0 ? 0u : 2u;          // (0,0): none; (0,j): up
     if (j == 0) return 4u;                         // (i,0): left
     const int64_t g = (j - 1) >> 6, l = (j - 1) & 63, q = (i - 1) >> 3, s = (i - 1) & 7;
-    return (D[(g * NC + q) * 64 + l] >> (28 - 4 * s)) & 0xfu;
+    return (v.D[(g * v.NC + q) * 64 + l] >> (28 - 4 * s)) & 0xfu;
 }
 
 // Dense nibble packing for nw_fill(): byte b = code(2b) | code(2b+1) << 4.
-__global__ void nw_pack_nibbles_kernel(const uint32_t* D, int32_t NC, int32_t L1, int32_t L2, uint8_t* out) {
+__global__ void nw_pack_nibbles_kernel(TableView v, int32_t L1, int32_t L2, uint8_t* out) {
     const int64_t N = (int64_t)L2 + 1;
     const int64_t ncell = ((int64_t)L1 + 1) * N;
     const int64_t nbyte = (ncell + 1) / 2;
     for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nbyte;
          b += (int64_t)gridDim.x * blockDim.x) {
         const int64_t c0 = 2 * b, c1 = 2 * b + 1;
-        uint32_t v = code_at(D, NC, c0 / N, c0 % N);
-        if (c1 < ncell) v |= code_at(D, NC, c1 / N, c1 % N) << 4;
-        out[b] = (uint8_t)v;
+        uint32_t x = code_at(v, c0 / N, c0 % N);
+        if (c1 < ncell) x |= code_at(v, c1 / N, c1 % N) << 4;
+        out[b] = (uint8_t)x;
     }
 }
 
 // One code byte per cell for columns [i0, i1).
-__global__ void nw_codes_kernel(const uint32_t* D, int32_t NC, int32_t L2, int64_t i0, int64_t i1, uint8_t* out) {
+__global__ void nw_codes_kernel(TableView v, int32_t L2, int64_t i0, int64_t i1, uint8_t* out) {
     const int64_t N = (int64_t)L2 + 1;
     const int64_t n = (i1 - i0) * N;
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n;
          x += (int64_t)gridDim.x * blockDim.x)
-        out[x] = (uint8_t)code_at(D, NC, i0 + x / N, x % N);
+        out[x] = (uint8_t)code_at(v, i0 + x / N, x % N);
 }
 
 // Per-column FNV-1a-64 of scores (int32 LE bytes) and codes (1 byte/cell).
-__global__ void nw_colhash_kernel(const int32_t* tiles, int64_t spitch, int32_t d, const uint32_t* D,
-                                  int32_t NC, int32_t L1,
-                                  int32_t L2, uint64_t* hcol, uint64_t* dcol) {
+__global__ void nw_colhash_kernel(TableView v, int32_t L1, int32_t L2, uint64_t* hcol, uint64_t* dcol) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i > L1) return;
     const uint64_t P = 0x100000001b3ULL;
     uint64_t h = 0xcbf29ce484222325ULL, e = 0xcbf29ce484222325ULL;
     for (int64_t j = 0; j <= L2; ++j) {
-        const uint32_t v = (uint32_t)score_at(tiles, spitch, d, i, j);
-        h = (h ^ (v & 0xff)) * P;
-        h = (h ^ ((v >> 8) & 0xff)) * P;
-        h = (h ^ ((v >> 16) & 0xff)) * P;
-        h = (h ^ (v >> 24)) * P;
-        if (D) e = (e ^ code_at(D, NC, i, j)) * P;
+        const uint32_t x = (uint32_t)score_at(v, i, j);
+        h = (h ^ (x & 0xff)) * P;
+        h = (h ^ ((x >> 8) & 0xff)) * P;
+        h = (h ^ ((x >> 16) & 0xff)) * P;
+        h = (h ^ (x >> 24)) * P;
+        if (v.D) e = (e ^ code_at(v, i, j)) * P;
     }
     hcol[i] = h;
     dcol[i] = e;
 }
 
 // --------------------------------------------------------------- host side
-thread_local std::string g_last_error;
-
-int fail(int rc, const std::string& msg) {
-    g_last_error = msg;
-    return rc;
-}
-
-#define HIPCHK(expr)                                                                        \
-    do {                                                                                    \
-        hipError_t e_ = (expr);                                                             \
-        if (e_ != hipSuccess)                                                               \
-            return fail(e_ == hipErrorOutOfMemory ? NW_ERR_OOM : NW_ERR_HIP,                \
-                        std::string(#expr) + ": " + hipGetErrorString(e_));                 \
-    } while (0)
-
 using KernelFn = void (*)(FillArgs);
 
 template <int W>
@@ -579,38 +627,169 @@ int choose_waves(int64_t NG, int ncu) {
     return 8;
 }
 
+TableView view_of(const nw_table* t) {
+    TableView v{};
+    v.tiles = t->H;
+    v.spitch = t->spitch;
+    v.D = (t->last_mask & NW_OUT_DIRS) ? t->D : nullptr;
+    v.NC = (int32_t)t->NC;
+    v.d = t->last_d;
+    v.row_base = (int32_t)t->row_base;
+    v.top = t->row_base > 0 ? t->xin : nullptr;
+    return v;
+}
 
 }  // namespace
 
-struct nw_table {
-    int device = 0;
-    int ncu = 256;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    uint32_t cap_mask = 0;
-    int64_t max_L1 = 0, max_L2 = 0;
-    // geometry for the current sequences
-    int64_t L1 = -1, L2 = -1;
-    int64_t NC = 0, NG = 0, spitch = 0;
-    // device buffers
-    uint8_t* s1 = nullptr;
-    uint8_t* s2 = nullptr;
-    int32_t* H = nullptr;       // score tiles (score_at)
-    uint32_t* D = nullptr;
-    int32_t* lastcol = nullptr;
-    uint64_t* gran = nullptr;
-    size_t gran_bytes = 0;
-    uint32_t* ctl = nullptr;
-    uint64_t* trace = nullptr;      // $NW_TRACE: in-kernel timeline
-    int64_t trace_n = 0;
-    // results of the last fill
-    bool filled = false;
-    uint32_t last_mask = 0;
-    int32_t last_d = 0;
-    nw_stats stats{};
-    float kernel_ms = 0.f, call_ms = 0.f;
-    int waves = 0;
-};
+namespace nwi {
+
+thread_local std::string g_last_error;
+
+int fail(int rc, const std::string& msg) {
+    g_last_error = msg;
+    return rc;
+}
+
+int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask) {
+    if (!t) return fail(NW_ERR_ARG, "nw_table_fill: NULL table");
+    if (t->L1 < 0) return fail(NW_ERR_STATE, "nw_table_fill: no sequences set");
+    if (t->launched) return fail(NW_ERR_STATE, "nw_table_fill: a fill is already in flight");
+    if ((out_mask & ~t->cap_mask & (NW_OUT_SCORES | NW_OUT_DIRS)) != 0)
+        return fail(NW_ERR_ARG, "nw_table_fill: output not allocated at creation");
+    // Overflow guard: |H| <= (L1+L2)*max(|m|,|k|,|d|); the shifted domain
+    // adds up to 64*W*|d| (W <= 16) and one more candidate term.
+    {
+        const int64_t M = std::max({std::llabs(m), std::llabs(k), std::llabs(d)});
+        const int64_t L2g = t->L2_total >= 0 ? t->L2_total : t->L2;
+        const int64_t bound = (t->L1 + L2g) * M + 1024 * std::llabs(d) + 2 * M + 2;
+        if (bound >= (int64_t)INT32_MAX)
+            return fail(NW_ERR_RANGE, "nw_table_fill: |scores| could reach " + std::to_string(bound));
+    }
+    NW_HIPCHK(hipSetDevice(t->device));
+    const bool sh = out_mask & NW_OUT_SCORES, sd = out_mask & NW_OUT_DIRS, stt = out_mask & NW_OUT_STATS;
+    const int64_t L1 = t->L1, L2 = t->L2;
+    const bool panel = t->xin || t->xout;
+    t->filled = false;
+    NW_HIPCHK(hipEventRecord(t->ev[0], t->stream));
+    NW_HIPCHK(hipMemsetAsync(t->ctl, 0, CTL_WORDS * 4, t->stream));
+    int W = 0;
+    if (L1 > 0 && L2 > 0) {
+        W = choose_waves(t->NG, t->ncu);
+        KernelFn fn = pick_kernel(W, sh, sd, stt);
+        if (!fn) return fail(NW_ERR_ARG, "nw_table_fill: unsupported wave count");
+        FillArgs a{};
+        a.s1 = t->s1;
+        a.s2 = t->s2;
+        a.L1 = (int32_t)L1;
+        a.L2 = (int32_t)L2;
+        a.m = m;
+        a.k = k;
+        a.d = d;
+        a.NC = (int32_t)t->NC;
+        a.NG = (int32_t)t->NG;
+        a.NSW = (int32_t)((t->NG + W - 1) / W);
+        a.H = t->H;
+        a.spitch = t->spitch;
+        a.D = t->D;
+        a.lastcol = t->lastcol;
+        a.gran = t->gran;
+        a.gpitch = CH * t->NC + CH;
+        a.ctl = t->ctl;
+        // A panel waits on another GPU (or process) that may start seconds
+        // later; a plain fill only on itself.
+        a.spin_ticks = t->xin ? 30 * SPIN_TICKS : SPIN_TICKS;
+        a.row_base = (int32_t)t->row_base;
+        a.epoch = t->epoch;
+        a.xin = t->xin;
+        a.xout = t->xout;
+        a.xflag = t->xflag;
+        a.xblk = (int32_t)std::max<int64_t>(t->xblk, 1);
+        if (t->xout && (L2 % 64) != 0) return fail(NW_ERR_ARG, "nw_table_fill: a feeding panel needs 64*k rows");
+        if (getenv("NW_TRACE")) {
+            const int64_t need = 4 * (int64_t)a.NSW;
+            if (t->trace_n < need) {
+                (void)hipFree(t->trace);
+                t->trace = nullptr;
+                t->trace_n = 0;
+                NW_HIPCHK(hipMalloc(&t->trace, (size_t)need * 8));
+                t->trace_n = need;
+            }
+            NW_HIPCHK(hipMemsetAsync(t->trace, 0, (size_t)need * 8, t->stream));
+            a.trace = t->trace;
+        }
+        int occ = 1;
+        NW_HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(fn), 64 * (W + 1), 0));
+        occ = std::max(occ, 1);
+        // A panel leaves room on every CU for the kernels of its neighbours
+        // and of the transport (RCCL), which its hand-off waits on.
+        const int per_cu = panel ? std::max(1, std::min(2, occ - 1)) : std::min(occ, 16);
+        const int64_t grid = std::min<int64_t>(a.NSW, (int64_t)t->ncu * per_cu);
+        a.nslot = (int32_t)std::min<int64_t>(grid + 1, (int64_t)(t->gran_bytes / 8 / a.gpitch));
+        if (a.nslot < grid + 1) return fail(NW_ERR_ARG, "nw_table_fill: granule buffer too small");
+        if (a.NSW > 1) NW_HIPCHK(hipMemsetAsync(t->gran, 0, (size_t)a.nslot * a.gpitch * 8, t->stream));
+        NW_HIPCHK(hipEventRecord(t->ev[1], t->stream));
+        void* kargs[] = {&a};
+        NW_HIPCHK(hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3((unsigned)grid), dim3(64 * (W + 1)), kargs,
+                                  0, t->stream));
+        NW_HIPCHK(hipGetLastError());
+        NW_HIPCHK(hipEventRecord(t->ev[2], t->stream));
+    } else {
+        NW_HIPCHK(hipEventRecord(t->ev[1], t->stream));
+        NW_HIPCHK(hipEventRecord(t->ev[2], t->stream));
+    }
+    t->launched = true;
+    t->pend_mask = out_mask;
+    t->pend_d = d;
+    t->pend_W = W;
+    return NW_OK;
+}
+
+int poison(uint64_t* p, int64_t n, uint32_t epoch, hipStream_t s) {
+    if (n <= 0) return NW_OK;
+    nw_poison_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, 1024), 256, 0, s>>>(p, n, epoch);
+    NW_HIPCHK(hipGetLastError());
+    return NW_OK;
+}
+
+int fill_finish(nw_table* t) {
+    if (!t || !t->launched) return fail(NW_ERR_STATE, "nw_table_fill: no fill in flight");
+    t->launched = false;
+    NW_HIPCHK(hipSetDevice(t->device));
+    const int64_t L1 = t->L1, L2 = t->L2;
+    const bool sh = t->pend_mask & NW_OUT_SCORES, stt = t->pend_mask & NW_OUT_STATS;
+    const int32_t d = t->pend_d;
+    NW_HIPCHK(hipEventRecord(t->ev[3], t->stream));
+    uint32_t ctl[CTL_WORDS];
+    NW_HIPCHK(hipMemcpyAsync(ctl, t->ctl, sizeof ctl, hipMemcpyDeviceToHost, t->stream));
+    int32_t corner = 0;
+    if (L1 > 0 && L2 > 0) {
+        const int64_t r = L2 - 1, q = L1 - 1;
+        const int32_t* src = sh ? t->H + (r >> 6) * t->spitch + (((q >> 2) * 64 + (r & 63)) << 2) + (q & 3)
+                                : t->lastcol + L2;
+        NW_HIPCHK(hipMemcpyAsync(&corner, src, 4, hipMemcpyDeviceToHost, t->stream));
+    }
+    NW_HIPCHK(hipStreamSynchronize(t->stream));
+    if (ctl[CTL_ERR])
+        return fail((int)ctl[CTL_ERR], (int)ctl[CTL_ERR] == NW_ERR_PEER
+                                           ? "nw_table_fill: the panel above failed"
+                                           : "nw_table_fill: in-kernel watchdog fired (hand-off timeout)");
+    NW_HIPCHK(hipEventElapsedTime(&t->kernel_ms, t->ev[1], t->ev[2]));
+    NW_HIPCHK(hipEventElapsedTime(&t->call_ms, t->ev[0], t->ev[3]));
+    if (L1 == 0 || L2 == 0) corner = (int32_t)(-(L1 + L2 + t->row_base) * (int64_t)d);
+    t->stats.corner = corner;
+    t->stats.greatest_abs_interior = stt ? (int32_t)ctl[CTL_GAV] : 0;
+    t->stats.branch_count = stt ? ctl[CTL_BC] : 0u;
+    t->filled = true;
+    t->last_mask = t->pend_mask;
+    t->last_d = d;
+    t->waves = t->pend_W;
+    return NW_OK;
+}
+
+}  // namespace nwi
+
+using nwi::fail;
+#define HIPCHK NW_HIPCHK
 
 extern "C" {
 
@@ -624,11 +803,12 @@ const char* nw_strerror(int rc) {
         case NW_ERR_RANGE: return "scores may overflow int32 for these inputs";
         case NW_ERR_TIMEOUT: return "device hand-off timed out";
         case NW_ERR_STATE: return "call out of order";
+        case NW_ERR_PEER: return "a peer panel failed";
         default: return "unknown error";
     }
 }
 
-const char* nw_last_error(void) { return g_last_error.c_str(); }
+const char* nw_last_error(void) { return nwi::g_last_error.c_str(); }
 
 void nw_table_destroy(nw_table* t) {
     if (!t) return;
@@ -730,103 +910,9 @@ int nw_table_set_sequences(nw_table* t, const char* s1, int64_t L1, const char* 
 }
 
 int nw_table_fill(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask) {
-    if (!t) return fail(NW_ERR_ARG, "nw_table_fill: NULL table");
-    if (t->L1 < 0) return fail(NW_ERR_STATE, "nw_table_fill: no sequences set");
-    if ((out_mask & ~t->cap_mask & (NW_OUT_SCORES | NW_OUT_DIRS)) != 0)
-        return fail(NW_ERR_ARG, "nw_table_fill: output not allocated at creation");
-    // Overflow guard: |H| <= (L1+L2)*max(|m|,|k|,|d|); the shifted domain
-    // adds up to 64*W*|d| (W <= 16) and one more candidate term.
-    {
-        const int64_t M = std::max({std::llabs(m), std::llabs(k), std::llabs(d)});
-        const int64_t bound = (t->L1 + t->L2) * M + 1024 * std::llabs(d) + 2 * M + 2;
-        if (bound >= (int64_t)INT32_MAX)
-            return fail(NW_ERR_RANGE, "nw_table_fill: |scores| could reach " + std::to_string(bound));
-    }
-    HIPCHK(hipSetDevice(t->device));
-    const bool sh = out_mask & NW_OUT_SCORES, sd = out_mask & NW_OUT_DIRS, stt = out_mask & NW_OUT_STATS;
-    const int64_t L1 = t->L1, L2 = t->L2;
-    HIPCHK(hipEventRecord(t->ev[0], t->stream));
-    HIPCHK(hipMemsetAsync(t->ctl, 0, CTL_WORDS * 4, t->stream));
-    HIPCHK(hipGetLastError());
-    int W = 0;
-    if (L1 > 0 && L2 > 0) {
-        W = choose_waves(t->NG, t->ncu);
-        KernelFn fn = pick_kernel(W, sh, sd, stt);
-        if (!fn) return fail(NW_ERR_ARG, "nw_table_fill: unsupported wave count");
-        FillArgs a{};
-        a.s1 = t->s1;
-        a.s2 = t->s2;
-        a.L1 = (int32_t)L1;
-        a.L2 = (int32_t)L2;
-        a.m = m;
-        a.k = k;
-        a.d = d;
-        a.NC = (int32_t)t->NC;
-        a.NG = (int32_t)t->NG;
-        a.NSW = (int32_t)((t->NG + W - 1) / W);
-        a.H = t->H;
-        a.spitch = t->spitch;
-        a.D = t->D;
-        a.lastcol = t->lastcol;
-        a.gran = t->gran;
-        a.gpitch = CH * t->NC + CH;
-        a.ctl = t->ctl;
-        if (getenv("NW_TRACE")) {
-            const int64_t need = 4 * (int64_t)a.NSW;
-            if (t->trace_n < need) {
-                (void)hipFree(t->trace);
-                t->trace = nullptr;
-                t->trace_n = 0;
-                HIPCHK(hipMalloc(&t->trace, (size_t)need * 8));
-                t->trace_n = need;
-            }
-            HIPCHK(hipMemsetAsync(t->trace, 0, (size_t)need * 8, t->stream));
-            a.trace = t->trace;
-        }
-        int occ = 1;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(fn), 64 * (W + 1), 0));
-        occ = std::max(occ, 1);
-        const int64_t grid = std::min<int64_t>(a.NSW, (int64_t)t->ncu * std::min(occ, 16));
-        a.nslot = (int32_t)std::min<int64_t>(grid + 1, (int64_t)(t->gran_bytes / 8 / a.gpitch));
-        if (a.nslot < grid + 1) return fail(NW_ERR_ARG, "nw_table_fill: granule buffer too small");
-        if (a.NSW > 1)
-            HIPCHK(hipMemsetAsync(t->gran, 0, (size_t)a.nslot * a.gpitch * 8, t->stream));
-        HIPCHK(hipEventRecord(t->ev[1], t->stream));
-        void* kargs[] = {&a};
-        HIPCHK(hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3((unsigned)grid), dim3(64 * (W + 1)), kargs, 0,
-                               t->stream));
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(t->ev[2], t->stream));
-    } else {
-        HIPCHK(hipEventRecord(t->ev[1], t->stream));
-        HIPCHK(hipEventRecord(t->ev[2], t->stream));
-    }
-    HIPCHK(hipEventRecord(t->ev[3], t->stream));
-    uint32_t ctl[CTL_WORDS];
-    HIPCHK(hipMemcpyAsync(ctl, t->ctl, sizeof ctl, hipMemcpyDeviceToHost, t->stream));
-    int32_t corner = 0;
-    if (L1 > 0 && L2 > 0) {
-        const int64_t r = L2 - 1, q = L1 - 1;
-        const int32_t* src = sh ? t->H + (r >> 6) * t->spitch + (((q >> 2) * 64 + (r & 63)) << 2) + (q & 3)
-                                : t->lastcol + L2;
-        HIPCHK(hipMemcpyAsync(&corner, src, 4, hipMemcpyDeviceToHost, t->stream));
-    }
-    HIPCHK(hipStreamSynchronize(t->stream));
-    if (ctl[CTL_ERR]) {
-        t->filled = false;
-        return fail((int)ctl[CTL_ERR], "nw_table_fill: in-kernel watchdog fired (hand-off timeout)");
-    }
-    HIPCHK(hipEventElapsedTime(&t->kernel_ms, t->ev[1], t->ev[2]));
-    HIPCHK(hipEventElapsedTime(&t->call_ms, t->ev[0], t->ev[3]));
-    if (L1 == 0 || L2 == 0) corner = (int32_t)(-(L1 + L2) * (int64_t)d);
-    t->stats.corner = corner;
-    t->stats.greatest_abs_interior = stt ? (int32_t)ctl[CTL_GAV] : 0;
-    t->stats.branch_count = stt ? ctl[CTL_BC] : 0u;
-    t->filled = true;
-    t->last_mask = out_mask;
-    t->last_d = d;
-    t->waves = W;
-    return NW_OK;
+    const int rc = nwi::fill_launch(t, m, k, d, out_mask);
+    if (rc) return rc;
+    return nwi::fill_finish(t);
 }
 
 int nw_table_stats(nw_table* t, nw_stats* st) {
@@ -865,7 +951,7 @@ static int copy_scores_impl(nw_table* t, int64_t i0, int64_t i1, int32_t* dst) {
     hipError_t e = hipSuccess;
     for (int64_t c0 = i0; c0 < i1 && e == hipSuccess; c0 += cols_per) {
         const int64_t c1 = std::min(i1, c0 + cols_per);
-        nw_gather_scores_kernel<<<1024, 256, 0, t->stream>>>(t->H, t->spitch, t->last_d, (int32_t)t->L2, c0, c1, stage);
+        nw_gather_scores_kernel<<<1024, 256, 0, t->stream>>>(view_of(t), (int32_t)t->L2, c0, c1, stage);
         e = hipGetLastError();
         if (e == hipSuccess)
             e = hipMemcpyAsync(dst + (c0 - i0) * N, stage, (size_t)((c1 - c0) * N * 4), hipMemcpyDeviceToHost, t->stream);
@@ -890,13 +976,24 @@ int nw_table_copy_last_column(nw_table* t, int32_t* dst) {
     if (!t->filled) return fail(NW_ERR_STATE, "nw_table_copy_last_column: no completed fill");
     HIPCHK(hipSetDevice(t->device));
     if (t->last_mask & NW_OUT_SCORES) return copy_scores_impl(t, t->L1, t->L1 + 1, dst);
-    if (t->L2 == 0 || t->L1 == 0) {
-        for (int64_t j = 0; j <= t->L2; ++j) dst[j] = (int32_t)(-(t->L1 + j) * (int64_t)t->last_d);
+    const int64_t d = t->last_d;
+    if (t->L1 == 0) {
+        for (int64_t j = 0; j <= t->L2; ++j) dst[j] = (int32_t)(-(t->row_base + j) * d);
         return NW_OK;
     }
-    HIPCHK(hipMemcpyAsync(dst + 1, t->lastcol + 1, (size_t)t->L2 * 4, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
-    dst[0] = (int32_t)(-t->L1 * (int64_t)t->last_d);
+    // Row 0: the seed, or (panels) the last row of the panel above.
+    if (t->row_base > 0) {
+        uint64_t g = 0;
+        HIPCHK(hipMemcpyAsync(&g, t->xin + (t->L1 - 1), 8, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(hipStreamSynchronize(t->stream));
+        dst[0] = (int32_t)(uint32_t)g + t->last_d;
+    } else {
+        dst[0] = (int32_t)(-t->L1 * d);
+    }
+    if (t->L2 > 0) {
+        HIPCHK(hipMemcpyAsync(dst + 1, t->lastcol + 1, (size_t)t->L2 * 4, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(hipStreamSynchronize(t->stream));
+    }
     return NW_OK;
 }
 
@@ -909,7 +1006,7 @@ int nw_table_copy_codes(nw_table* t, int64_t i0, int64_t i1, uint8_t* dst) {
     const size_t n = (size_t)((i1 - i0) * (t->L2 + 1));
     uint8_t* buf = nullptr;
     HIPCHK(hipMalloc(&buf, n));
-    nw_codes_kernel<<<1024, 256, 0, t->stream>>>(t->D, (int32_t)t->NC, (int32_t)t->L2, i0, i1, buf);
+    nw_codes_kernel<<<1024, 256, 0, t->stream>>>(view_of(t), (int32_t)t->L2, i0, i1, buf);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(dst, buf, n, hipMemcpyDeviceToHost, t->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(t->stream);
@@ -926,9 +1023,10 @@ int nw_table_hash(nw_table* t, uint64_t* hH, uint64_t* hD) {
     uint64_t* dh = nullptr;
     HIPCHK(hipMalloc(&dh, (size_t)ncol * 16));
     const bool have_d = (t->last_mask & NW_OUT_DIRS) != 0;
-    nw_colhash_kernel<<<(unsigned)((ncol + 255) / 256), 256, 0, t->stream>>>(
-        t->H, t->spitch, t->last_d, have_d ? t->D : nullptr, (int32_t)t->NC, (int32_t)t->L1, (int32_t)t->L2, dh,
-        dh + ncol);
+    TableView v = view_of(t);
+    if (!have_d) v.D = nullptr;
+    nw_colhash_kernel<<<(unsigned)((ncol + 255) / 256), 256, 0, t->stream>>>(v, (int32_t)t->L1, (int32_t)t->L2, dh,
+                                                                              dh + ncol);
     std::vector<uint64_t> hv((size_t)ncol * 2);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpyAsync(hv.data(), dh, (size_t)ncol * 16, hipMemcpyDeviceToHost, t->stream);
@@ -964,8 +1062,8 @@ int nw_fill(const char* s1, int64_t L1, const char* s2, int64_t L2, int32_t m, i
         uint8_t* buf = nullptr;
         if (hipMalloc(&buf, nbyte) != hipSuccess) rc = fail(NW_ERR_OOM, "nw_fill: hipMalloc(dirs)");
         if (!rc) {
-            hipLaunchKernelGGL(nw_pack_nibbles_kernel, dim3(1024), dim3(256), 0, t->stream, t->D, (int32_t)t->NC,
-                               (int32_t)L1, (int32_t)L2, buf);
+            hipLaunchKernelGGL(nw_pack_nibbles_kernel, dim3(1024), dim3(256), 0, t->stream, view_of(t), (int32_t)L1,
+                               (int32_t)L2, buf);
             hipError_t e = hipGetLastError();
             if (e == hipSuccess) e = hipMemcpyAsync(dirs, buf, nbyte, hipMemcpyDeviceToHost, t->stream);
             if (e == hipSuccess) e = hipStreamSynchronize(t->stream);

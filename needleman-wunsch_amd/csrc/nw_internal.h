@@ -1,0 +1,78 @@
+// nw_internal.h -- state shared by nw_fill.hip (single-GPU table) and
+// nw_panel.hip (row panels across GPUs).  Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "nw_fill.h"
+
+struct nw_table {
+    int device = 0;
+    int ncu = 256;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint32_t cap_mask = 0;
+    int64_t max_L1 = 0, max_L2 = 0;
+    // geometry for the current sequences
+    int64_t L1 = -1, L2 = -1;
+    int64_t NC = 0, NG = 0, spitch = 0;
+    // device buffers
+    uint8_t* s1 = nullptr;
+    uint8_t* s2 = nullptr;
+    int32_t* H = nullptr;       // score tiles (score_at)
+    uint32_t* D = nullptr;
+    int32_t* lastcol = nullptr;
+    uint64_t* gran = nullptr;
+    size_t gran_bytes = 0;
+    uint32_t* ctl = nullptr;
+    uint64_t* trace = nullptr;      // $NW_TRACE: in-kernel timeline
+    int64_t trace_n = 0;
+    // Row-panel hand-off (set by nw_panel.hip; all null for a plain table).
+    int64_t row_base = 0;           // global row of local row 0
+    int64_t L2_total = -1;          // global rows, for the overflow guard (-1: L2)
+    const uint64_t* xin = nullptr;  // top boundary granules (device), or null
+    uint64_t* xout = nullptr;       // bottom boundary granules (device, maybe a peer's xin)
+    uint32_t* xflag = nullptr;      // host-visible block flags, or null
+    int64_t xblk = 0;               // chunks per hand-off block
+    uint32_t epoch = 0;             // tag of the fill in flight
+    // fill in flight (between fill_launch and fill_finish)
+    bool launched = false;
+    uint32_t pend_mask = 0;
+    int32_t pend_d = 0;
+    int pend_W = 0;
+    // results of the last fill
+    bool filled = false;
+    uint32_t last_mask = 0;
+    int32_t last_d = 0;
+    nw_stats stats{};
+    float kernel_ms = 0.f, call_ms = 0.f;
+    int waves = 0;
+};
+
+namespace nwi {
+
+int fail(int rc, const std::string& msg);
+
+// Enqueue one fill on t->stream (no host synchronisation), then complete it.
+// nw_table_fill() is fill_launch + fill_finish; panels run their boundary
+// transport in between.
+int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask);
+int fill_finish(nw_table* t);
+
+// Write "producer failed" granules for `epoch` over p[0, n) (any device memory,
+// including a peer's mapped boundary buffer), on stream s.
+int poison(uint64_t* p, int64_t n, uint32_t epoch, hipStream_t s);
+
+constexpr int kChunk = 8;   // columns per chunk (hand-off granules per chunk)
+
+}  // namespace nwi
+
+#define NW_HIPCHK(expr)                                                                     \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return nwi::fail(e_ == hipErrorOutOfMemory ? NW_ERR_OOM : NW_ERR_HIP,           \
+                             std::string(#expr) + ": " + hipGetErrorString(e_));            \
+    } while (0)

@@ -1,4 +1,5 @@
-"""Python binding (ctypes) of the MI355X Needleman-Wunsch fill, include/nw_fill.h.
+"""Python binding (ctypes) of the MI355X Needleman-Wunsch fill, include/nw_fill.h
+and include/nw_panel.h.
 
 This mirrors the reference's hot-path seam -- ``compute_table_scores(C)``
 (needleman-wunsch.c:583-626), called once per alignment by the driver at
@@ -7,7 +8,9 @@ needleman-wunsch.c:662 -- as two entry points:
 * :func:`fill` -- one-shot fill into host arrays (scores, direction codes,
   stats), what the CLI's traceback/printer consume;
 * :class:`Table` -- a device-resident table (the 100k x 100k path: the table
-  stays in HBM; hashes, slices and stats are pulled on demand).
+  stays in HBM; hashes, slices and stats are pulled on demand);
+* :class:`Panel` -- one row panel of a table split across GPUs (one process
+  per GPU over hipIpc or RCCL, or an in-process group).
 
 The library is required: importing works without it (so CPU-only tooling can
 inspect the module), but every call raises :class:`NWError` when
@@ -38,6 +41,14 @@ NW_ERR_HIP = -4
 NW_ERR_RANGE = -5
 NW_ERR_TIMEOUT = -6
 NW_ERR_STATE = -7
+NW_ERR_PEER = -8
+
+NW_PANEL_GROUP = 0
+NW_PANEL_IPC = 1
+NW_PANEL_RCCL = 2
+PANEL_ID_BYTES = 256
+PANEL_IPC_BYTES = 64
+PANEL_REC = 8
 
 # Exported symbols of include/nw_fill.h (checked by tests/test_abi.py).
 EXPORTS = (
@@ -46,6 +57,11 @@ EXPORTS = (
     "nw_table_stats", "nw_table_elapsed_ms", "nw_table_hash", "nw_table_copy_scores",
     "nw_table_copy_codes", "nw_table_copy_last_column", "nw_table_score_pitch", "nw_table_waves",
     "nw_table_trace",
+    # include/nw_panel.h
+    "nw_panel_partition", "nw_panel_chain", "nw_panel_get_id", "nw_panel_create", "nw_panel_ipc_handle",
+    "nw_panel_ipc_connect", "nw_panel_group_create", "nw_panel_destroy", "nw_panel_set_sequences",
+    "nw_panel_fill", "nw_panel_group_fill", "nw_panel_stats", "nw_panel_record", "nw_panel_reduce",
+    "nw_panel_rows", "nw_panel_table", "nw_panel_elapsed_ms",
 )
 
 
@@ -112,6 +128,30 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.nw_table_trace.argtypes = [c_p, c_p, c_i64]
     lib.nw_table_waves.restype = ctypes.c_int
     lib.nw_table_waves.argtypes = [c_p]
+    c_int, P = ctypes.c_int, ctypes.POINTER
+    sigs = {
+        "nw_panel_partition": (c_int, [c_i64, c_int, c_int, P(c_i64), P(c_i64)]),
+        "nw_panel_chain": (c_int, [c_i64, c_int, c_int, P(c_int), P(c_int), P(c_int)]),
+        "nw_panel_get_id": (c_int, [c_p]),
+        "nw_panel_create": (c_int, [c_int, c_int, c_int, c_int, c_p, c_i64, c_i64, c_u32, P(c_p)]),
+        "nw_panel_ipc_handle": (c_int, [c_p, c_p]),
+        "nw_panel_ipc_connect": (c_int, [c_p, c_p]),
+        "nw_panel_group_create": (c_int, [c_int, c_p, c_i64, c_i64, c_u32, c_p]),
+        "nw_panel_destroy": (None, [c_p]),
+        "nw_panel_set_sequences": (c_int, [c_p, ctypes.c_char_p, c_i64, ctypes.c_char_p, c_i64]),
+        "nw_panel_fill": (c_int, [c_p, c_i32, c_i32, c_i32, c_u32]),
+        "nw_panel_group_fill": (c_int, [c_p, c_int, c_i32, c_i32, c_i32, c_u32]),
+        "nw_panel_stats": (c_int, [c_p, P(_Stats)]),
+        "nw_panel_record": (c_int, [c_p, c_p]),
+        "nw_panel_reduce": (c_int, [c_p, c_int, P(_Stats)]),
+        "nw_panel_rows": (c_int, [c_p, P(c_i64), P(c_i64)]),
+        "nw_panel_table": (c_p, [c_p]),
+        "nw_panel_elapsed_ms": (c_int, [c_p, P(ctypes.c_float), P(ctypes.c_float)]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
     _lib = lib
     return lib
 
@@ -164,14 +204,25 @@ class Table:
     def __init__(self, max_L1: int, max_L2: int, out_mask: int = NW_OUT_ALL, device: int = -1):
         self._lib = load()
         self._h = ctypes.c_void_p()
+        self._owned = True
         _check(self._lib.nw_table_create(device, max_L1, max_L2, out_mask, ctypes.byref(self._h)),
                "nw_table_create")
         self.L1 = self.L2 = None
 
+    @classmethod
+    def _borrow(cls, handle, L1: int, L2: int) -> "Table":
+        """A view of a table owned elsewhere (a panel's local rows)."""
+        t = cls.__new__(cls)
+        t._lib = load()
+        t._h = ctypes.c_void_p(handle)
+        t._owned = False
+        t.L1, t.L2 = L1, L2
+        return t
+
     def close(self) -> None:
-        if self._h:
+        if self._h and self._owned:
             self._lib.nw_table_destroy(self._h)
-            self._h = ctypes.c_void_p()
+        self._h = ctypes.c_void_p()
 
     def __enter__(self):
         return self
@@ -242,6 +293,139 @@ class Table:
     @property
     def score_pitch(self) -> int:
         return self._lib.nw_table_score_pitch(self._h)
+
+
+# ------------------------------------------------------------------ panels
+def panel_partition(L2: int, nranks: int, rank: int):
+    """(row_base, rows) of `rank`'s panel (include/nw_panel.h)."""
+    lib = load()
+    b, n = ctypes.c_int64(), ctypes.c_int64()
+    _check(lib.nw_panel_partition(L2, nranks, rank, ctypes.byref(b), ctypes.byref(n)), "nw_panel_partition")
+    return b.value, n.value
+
+
+def panel_chain(L2: int, nranks: int, rank: int):
+    """(prev, next, pos) of `rank` in the boundary-row chain (-1 = none)."""
+    lib = load()
+    a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    _check(lib.nw_panel_chain(L2, nranks, rank, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+           "nw_panel_chain")
+    return a.value, b.value, c.value
+
+
+def panel_get_id() -> bytes:
+    """RCCL rendezvous id (rank 0 creates, every rank passes it to Panel)."""
+    lib = load()
+    buf = (ctypes.c_uint8 * PANEL_ID_BYTES)()
+    _check(lib.nw_panel_get_id(buf), "nw_panel_get_id")
+    return bytes(buf)
+
+
+def panel_reduce(records) -> tuple[int, Stats]:
+    """Whole-table stats from every rank's record; returns (rc, Stats)."""
+    lib = load()
+    recs = np.ascontiguousarray(np.asarray(records, dtype=np.int64).reshape(-1, PANEL_REC))
+    st = _Stats()
+    rc = lib.nw_panel_reduce(recs.ctypes.data, recs.shape[0], ctypes.byref(st))
+    return rc, Stats(st.corner, st.greatest_abs_interior, st.branch_count)
+
+
+class Panel:
+    """One row panel of a table split across GPUs (include/nw_panel.h)."""
+
+    def __init__(self, transport: int, rank: int, nranks: int, max_L1: int, max_L2: int,
+                 out_mask: int = NW_OUT_ALL, device: int = -1, rdv_id: bytes | None = None, _handle=None):
+        self._lib = load()
+        self._h = ctypes.c_void_p()
+        self.rank, self.nranks = rank, nranks
+        self.L1 = self.L2 = None
+        if _handle is not None:
+            self._h = ctypes.c_void_p(_handle)
+            return
+        idbuf = None
+        if rdv_id is not None:
+            idbuf = (ctypes.c_uint8 * PANEL_ID_BYTES).from_buffer_copy(rdv_id)
+        _check(self._lib.nw_panel_create(transport, device, rank, nranks, idbuf, max_L1, max_L2, out_mask,
+                                         ctypes.byref(self._h)), "nw_panel_create")
+
+    @classmethod
+    def group(cls, devices, max_L1: int, max_L2: int, out_mask: int = NW_OUT_ALL) -> list["Panel"]:
+        lib = load()
+        n = len(devices)
+        devs = (ctypes.c_int * n)(*devices)
+        hs = (ctypes.c_void_p * n)()
+        _check(lib.nw_panel_group_create(n, devs, max_L1, max_L2, out_mask, hs), "nw_panel_group_create")
+        return [cls(NW_PANEL_GROUP, r, n, 0, 0, _handle=hs[r]) for r in range(n)]
+
+    @staticmethod
+    def group_fill(panels, m: int, k: int, d: int, out_mask: int = NW_OUT_SCORES | NW_OUT_DIRS) -> None:
+        lib = load()
+        hs = (ctypes.c_void_p * len(panels))(*[p._h.value for p in panels])
+        _check(lib.nw_panel_group_fill(hs, len(panels), m, k, d, out_mask), "nw_panel_group_fill")
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.nw_panel_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def ipc_handle(self) -> bytes:
+        buf = (ctypes.c_uint8 * PANEL_IPC_BYTES)()
+        _check(self._lib.nw_panel_ipc_handle(self._h, buf), "nw_panel_ipc_handle")
+        return bytes(buf)
+
+    def ipc_connect(self, handles: bytes) -> None:
+        assert len(handles) == self.nranks * PANEL_IPC_BYTES
+        buf = (ctypes.c_uint8 * len(handles)).from_buffer_copy(handles)
+        _check(self._lib.nw_panel_ipc_connect(self._h, buf), "nw_panel_ipc_connect")
+
+    def set_sequences(self, s1, s2) -> None:
+        b1, b2 = _bytes(s1), _bytes(s2)
+        _check(self._lib.nw_panel_set_sequences(self._h, b1, len(b1), b2, len(b2)), "nw_panel_set_sequences")
+        self.L1, self.L2 = len(b1), len(b2)
+
+    def fill(self, m: int, k: int, d: int, out_mask: int = NW_OUT_SCORES | NW_OUT_DIRS) -> None:
+        _check(self._lib.nw_panel_fill(self._h, m, k, d, out_mask), "nw_panel_fill")
+
+    def fill_rc(self, m: int, k: int, d: int, out_mask: int = NW_OUT_SCORES | NW_OUT_DIRS) -> int:
+        return self._lib.nw_panel_fill(self._h, m, k, d, out_mask)
+
+    def record(self) -> np.ndarray:
+        rec = np.zeros(PANEL_REC, dtype=np.int64)
+        _check(self._lib.nw_panel_record(self._h, rec.ctypes.data), "nw_panel_record")
+        return rec
+
+    def stats(self) -> Stats:
+        st = _Stats()
+        _check(self._lib.nw_panel_stats(self._h, ctypes.byref(st)), "nw_panel_stats")
+        return Stats(st.corner, st.greatest_abs_interior, st.branch_count)
+
+    def rows(self):
+        b, n = ctypes.c_int64(), ctypes.c_int64()
+        _check(self._lib.nw_panel_rows(self._h, ctypes.byref(b), ctypes.byref(n)), "nw_panel_rows")
+        return b.value, n.value
+
+    @property
+    def table(self) -> Table:
+        """The panel's local rows (local row j = global row row_base + j)."""
+        _, rows = self.rows()
+        return Table._borrow(self._lib.nw_panel_table(self._h), self.L1, rows)
+
+    def elapsed_ms(self):
+        a, b = ctypes.c_float(), ctypes.c_float()
+        _check(self._lib.nw_panel_elapsed_ms(self._h, ctypes.byref(a), ctypes.byref(b)), "nw_panel_elapsed_ms")
+        return a.value, b.value
 
 
 # ----------------------------------------------------------------- inputs

@@ -131,6 +131,48 @@ int nwo_fill(const char *s1, int64_t L1, const char *s2, int64_t L2,
         return 0;
 }
 
+/* A band of rows (a multi-GPU row panel, include/nw_panel.h): global rows
+ * row_base+1 .. row_base+rows, given the global row row_base above it as
+ * top[0..L1].  The same recurrence (needleman-wunsch.c:418-510); column 0 is
+ * the seed -j*d (computation.c:112-120) at global row j.  H is
+ * (L1+1)*(rows+1) i-major with local row 0 = top; D (nullable) the codes of
+ * local rows >= 1 (row 0: 0, it belongs to the band above).  Stats cover the
+ * band's own interior cells.  s2 points at the band's first side-string byte. */
+int nwo_fill_band(const char *s1, int64_t L1, const char *s2, int64_t rows, int64_t row_base,
+                  const int32_t *top, int32_t m, int32_t k, int32_t d,
+                  int32_t *H, uint8_t *D, nwo_stats *st)
+{
+        const int64_t N = rows + 1;
+        int32_t gav = 0;
+        uint32_t bc = 0;
+        for (int64_t j = 0; j <= rows; j++) {
+                H[j] = wmul(row_base + j, wsub(0, d));
+                if (D) D[j] = j ? 2 : 0;
+        }
+        for (int64_t i = 1; i <= L1; i++) {
+                int32_t *cur = H + i * N;
+                const int32_t *prev = H + (i - 1) * N;
+                cur[0] = top[i];
+                if (D) D[i * N] = 0;
+                const char a = s1[i - 1];
+                for (int64_t j = 1; j <= rows; j++) {
+                        uint8_t c;
+                        int32_t h = cell(cur[j - 1], prev[j - 1], prev[j], a == s2[j - 1], m, k, d, &c);
+                        cur[j] = h;
+                        if (D) D[i * N + j] = c;
+                        bc += popc3(c) > 1;
+                        int32_t ah = iabs32(h);
+                        if (ah > gav) gav = ah;
+                }
+        }
+        if (st) {
+                st->corner = H[L1 * N + rows];
+                st->greatest_abs_interior = gav;
+                st->branch_count = bc;
+        }
+        return 0;
+}
+
 int nwo_fill_hash(const char *s1, int64_t L1, const char *s2, int64_t L2,
                   int32_t m, int32_t k, int32_t d,
                   uint64_t *hH, uint64_t *hD, nwo_stats *st)

@@ -38,6 +38,13 @@ int nwo_fill(const char *s1, int64_t L1, const char *s2, int64_t L2,
              int32_t m, int32_t k, int32_t d,
              int32_t *H, uint8_t *D, nwo_stats *st);
 
+/* Row band (multi-GPU panel) given the row above it, top[0..L1]; H is
+ * (L1+1)*(rows+1) with local row 0 = top, D codes (row 0: 0), stats over the
+ * band's interior.  s2 = the band's side-string bytes. */
+int nwo_fill_band(const char *s1, int64_t L1, const char *s2, int64_t rows, int64_t row_base,
+                  const int32_t *top, int32_t m, int32_t k, int32_t d,
+                  int32_t *H, uint8_t *D, nwo_stats *st);
+
 /* Streaming fill in O(L2) memory: FNV-1a-64 of the score table (int32 LE)
  * and of the code bytes, in i-major order, plus the stats. */
 int nwo_fill_hash(const char *s1, int64_t L1, const char *s2, int64_t L2,

@@ -42,6 +42,8 @@ def lib():
         L.nwo_fill_mt.argtypes = [ctypes.c_char_p, i64, ctypes.c_char_p, i64, i32, i32, i32, p, p,
                                   ctypes.POINTER(Stats), ctypes.c_int]
         L.nwo_gen_dna.argtypes = [ctypes.c_uint64, i64, ctypes.c_char_p]
+        L.nwo_fill_band.argtypes = [ctypes.c_char_p, i64, ctypes.c_char_p, i64, i64, p, i32, i32, i32, p, p,
+                                    ctypes.POINTER(Stats)]
         _lib = L
     return _lib
 
@@ -65,6 +67,20 @@ def fill(s1, s2, m, k, d, codes=True):
     st = Stats()
     lib().nwo_fill(s1, L1, s2, L2, m, k, d, H.ctypes.data, D.ctypes.data if codes else None,
                    ctypes.byref(st))
+    return H, D, (st.corner, st.gav, st.bc)
+
+
+def fill_band(s1, s2_band, row_base, top, m, k, d):
+    """Row band given the row above it (top: L1+1 int32 of global row row_base).
+    Returns (H (L1+1, rows+1) with row 0 = top, codes (row 0 = 0), (corner, gav, bc))."""
+    L1, rows = len(s1), len(s2_band)
+    top = np.ascontiguousarray(top, dtype=np.int32)
+    assert top.shape == (L1 + 1,)
+    H = np.empty((L1 + 1, rows + 1), dtype=np.int32)
+    D = np.empty((L1 + 1, rows + 1), dtype=np.uint8)
+    st = Stats()
+    lib().nwo_fill_band(s1, L1, s2_band, rows, row_base, top.ctypes.data, m, k, d, H.ctypes.data, D.ctypes.data,
+                        ctypes.byref(st))
     return H, D, (st.corner, st.gav, st.bc)
 
 

@@ -1,4 +1,4 @@
-"""The C ABI (include/nw_fill.h) -- CPU checks: the library loads, exports
+"""The C ABI (include/nw_fill.h, include/nw_panel.h) -- CPU checks: the library loads, exports
 every declared entry point, reports errors without exit()ing, and the
 Python binding mirrors it.  No GPU compute here."""
 import ctypes
@@ -12,13 +12,15 @@ from conftest import ROOT
 
 PKG = os.path.join(ROOT, "needleman-wunsch_amd")
 LIB = os.path.join(PKG, "lib", "libnwfill.so")
-HEADER = os.path.join(ROOT, "include", "nw_fill.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("nw_fill.h", "nw_panel.h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(nw_[a-z_]+)\s*\(", src)))
+    names = set()
+    for h in HEADERS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(nw_[a-z_]+)\s*\(", src))
+    return sorted(names)
 
 
 @pytest.fixture(scope="module")
@@ -30,7 +32,7 @@ def lib():
 
 def test_every_declared_symbol_is_exported(lib):
     names = declared_functions()
-    assert len(names) >= 15
+    assert len(names) >= 33
     for n in names:
         assert hasattr(lib, n), n
 
@@ -42,7 +44,7 @@ def test_python_binding_lists_every_export():
 
 def test_strerror_covers_codes(lib):
     lib.nw_strerror.restype = ctypes.c_char_p
-    for rc in range(0, -8, -1):
+    for rc in range(0, -9, -1):
         assert lib.nw_strerror(rc) and lib.nw_strerror(rc) != b"unknown error"
     assert lib.nw_strerror(-99) == b"unknown error"
 
@@ -54,13 +56,27 @@ def test_bad_arguments_return_error_codes(lib):
     assert lib.nw_table_create(0, -1, 5, 1, None) == -1
     lib.nw_table_fill.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32]
     assert lib.nw_table_fill(None, 1, 1, 1, 1) == -1
+    P = ctypes.POINTER
+    lib.nw_panel_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                    ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32, P(ctypes.c_void_p)]
+    h = ctypes.c_void_p()
+    assert lib.nw_panel_create(7, 0, 0, 2, None, 10, 10, 1, ctypes.byref(h)) == -1     # unknown transport
+    assert lib.nw_panel_create(2, 0, 0, 2, None, 10, 10, 1, ctypes.byref(h)) == -1     # RCCL needs an id
+    assert lib.nw_panel_create(1, 0, 2, 2, None, 10, 10, 1, ctypes.byref(h)) == -1     # rank >= nranks
+    lib.nw_panel_fill.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32]
+    assert lib.nw_panel_fill(None, 1, 1, 1, 1) == -1
+    lib.nw_panel_group_create.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                          ctypes.c_uint32, ctypes.c_void_p]
+    assert lib.nw_panel_group_create(0, None, 10, 10, 1, None) == -1
+    lib.nw_panel_table.restype = ctypes.c_void_p
+    assert lib.nw_panel_table(None) is None
 
 
 def test_device_code_is_gfx950_only():
     """The embedded offload bundle carries exactly one device target: gfx950."""
     data = open(LIB, "rb").read()
-    i = data.find(b"__CLANG_OFFLOAD_BUNDLE__")
-    assert i >= 0
-    header = data[i:i + 4096]
-    targets = re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", header)
-    assert targets == [b"gfx950"]
+    starts = [m.start() for m in re.finditer(rb"__CLANG_OFFLOAD_BUNDLE__", data)]
+    assert starts
+    for i in starts:   # one bundle per HIP source
+        targets = re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", data[i:i + 4096])
+        assert targets == [b"gfx950"]
