@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output of tools/profile_round.sh into profiles/.
+
+    python tools/pmc_traffic.py ROUND OUTDIR L1 L2
+
+OUTDIR holds three rocprofv3 runs of `bench.py` (same workload):
+  kt/   --kernel-trace --stats        -> per-kernel average duration
+  wr/   --pmc WRITE_SIZE              -> HBM write bytes per fill launch
+  rd/   --pmc FETCH_SIZE              -> HBM read bytes per fill launch
+Counters come from separate passes (TCC slots: FETCH_SIZE costs 3,
+WRITE_SIZE 2, MI355X_MICROARCH.md "rocprofv3 PMC slots").  Both are KiB
+(x1024).  gfx950 correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE reads
+half the bytes of a wide coalesced stream, so it is doubled; WRITE_SIZE is
+exact for 16-B/lane streaming stores (the score tiles).
+
+Writes OUTDIR/<ROUND>_kernel_stats.csv (copy of the stats summary) and
+OUTDIR/<ROUND>_pmc_traffic.json; commit both under profiles/ (bench.py reads
+profiles/*pmc*.json for roofline.traffic).
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+FILL = "nw_fill_kernel"
+
+
+def find(d, pattern):
+    hits = sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True))
+    if not hits:
+        raise SystemExit(f"no {pattern} under {d}")
+    return hits[-1]
+
+
+def counter_per_launch(d, name):
+    path = find(d, "*counter_collection.csv")
+    per = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if FILL not in r["Kernel_Name"] or r["Counter_Name"] != name:
+                continue
+            key = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+    if not per:
+        raise SystemExit(f"{name}: no fill-kernel rows in {path}")
+    vals = list(per.values())
+    return sum(vals) / len(vals), len(vals), os.path.relpath(path, ROOT)
+
+
+def main():
+    rnd, out, L1, L2 = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+    stats = find(os.path.join(out, "kt"), "*kernel_stats.csv")
+    dst = os.path.join(out, f"{rnd}_kernel_stats.csv")
+    shutil.copy(stats, dst)
+    avg_ns = None
+    with open(stats) as f:
+        for r in csv.DictReader(f):
+            if FILL in r["Name"]:
+                avg_ns = float(r["AverageNs"])
+                name = r["Name"]
+    wr_kib, nw, wsrc = counter_per_launch(os.path.join(out, "wr"), "WRITE_SIZE")
+    rd_kib, nr, rsrc = counter_per_launch(os.path.join(out, "rd"), "FETCH_SIZE")
+    write_b = wr_kib * 1024
+    fetch_b = 2 * rd_kib * 1024
+    alg = 4.5 * (L1 + 1) * (L2 + 1)
+    j = {
+        "round": rnd, "L1": L1, "L2": L2, "kernel": name, "avg_kernel_ns": avg_ns,
+        "write_bytes_per_launch": write_b, "fetch_bytes_per_launch": fetch_b,
+        "hbm_bytes_per_launch": write_b + fetch_b,
+        "alg_bytes_per_launch": alg, "traffic_over_alg": (write_b + fetch_b) / alg,
+        "hbm_gbs_from_counters": (write_b + fetch_b) / avg_ns if avg_ns else None,
+        "launches": {"WRITE_SIZE": nw, "FETCH_SIZE": nr},
+        "correction": "WRITE_SIZE*1024 + 2*FETCH_SIZE*1024 (gfx950 FETCH_SIZE halves wide streams)",
+        "sources": {"stats": f"profiles/{rnd}_kernel_stats.csv", "write": f"profiles/{rnd}_pmc_write_size.csv", "fetch": f"profiles/{rnd}_pmc_fetch_size.csv"},
+    }
+    with open(os.path.join(out, f"{rnd}_pmc_traffic.json"), "w") as f:
+        json.dump(j, f, indent=1)
+    print(json.dumps(j))
+
+
+if __name__ == "__main__":
+    main()
