@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
@@ -78,186 +79,100 @@ struct FillArgs {
 };
 
 // ---------------------------------------------------------------- DPP helpers
-// wave_shr:1 -- lane l receives lane l-1; lane 0 keeps `old`.
-__device__ __forceinline__ int wave_shr1(int old, int v) {
-    return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xf, 0xf, false);
-}
-
 typedef const __attribute__((address_space(4))) uint64_t* cptr64;
 
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4_t u32x4(int a, int b, int c, int d) {
-    return u32x4_t{(unsigned)a, (unsigned)b, (unsigned)c, (unsigned)d};
-}
 
-__device__ __forceinline__ int iabs(int v) { return v < 0 ? -v : v; }
-
-// Count nibbles of a codes word that have >= 2 of their 3 direction bits.
-__device__ __forceinline__ uint32_t branch_nibbles(uint32_t x) {
-    uint32_t y = (x & (x >> 1)) | (x & (x >> 2)) | ((x >> 1) & (x >> 2));
-    return __builtin_popcount(y & 0x11111111u);
+// LDS byte address of a __shared__ object (for ds_* in inline asm).
+__device__ __forceinline__ int lds_addr(const void* p) {
+    return (int)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
 // Wave-uniform copies of per-wave values (so address math stays scalar).
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// ------------------------------------------------------------ per-wave state
-struct WaveState {
-    int G;          // shifted score of this lane's row at the last column
-    int Tprev;      // lane -1 (row above the stripe) shifted score, last column
-    uint32_t c2;    // this lane's side-string byte
-    int laneoff;    // (64*w + lane) * d: H = G - laneoff
-    int gav;        // running max |H| (stats)
-    uint32_t bc;    // running branch count (stats)
-};
-
-// One 8-column chunk of one wave.  NSTEP is 8 except for the last chunk.
+// ------------------------------------------------------------ column steps
+// Domain.  A wave works on G' = H + r*d + (i - base)*d, r = row offset inside
+// the workgroup (64*w + lane), i = column, base = the column where the current
+// 4096-column "super-chunk" starts.  In it the left candidate H[i-1][j] - d is
+// G'_{i-1} itself, the diagonal is wave_shr1(G'_{i-1}) + sub + 2d, and the up
+// dependency becomes a prefix max over the lanes (DESIGN.md "Fill kernel"):
+//     G'_i = prefmax( max3(G'_{i-1}, wave_shr1(G'_{i-1}) + sub'_i, T'_i) ),
+//     sub' = match ? m + 2d : 2d - k,   T'_i = the row above, same domain.
+// base moves every 512 chunks so |G'| stays within |H| + (64W + 4104)|d|.
 // Cell recurrence = needleman-wunsch.c:429-465; direction flags :485-503.
-// ----------------------------------------------------------- step kernels
-// One column step of one wave, hand-scheduled.  The loop-carried chain is
-//   G --dpp wave_shr:1--> sh --add--> dg --max3(lf,dg,top)--> Y --6 x dpp max--> G'
-// and every DPP read of a VGPR written by the previous VALU needs two wait
-// states.  Instead of s_nop, those slots carry the *previous* step's
-// independent outputs: its direction code (3 compares, shifted into `acc`
-// with v_addc: acc = 16*acc + diag + 2*up + 4*left), its score H = G - laneoff
-// and (stats) the running max |H|.  The previous step's up candidate is this
-// step's `sh` (wave_shr:1 of G with lane 0 = row above), so it comes free.
-#define NW_STEP_HEAD                                                   \
-    "v_cmp_eq_u32_e32 vcc, %[ch], %[c2]\n\t"                           \
-    "v_cndmask_b32_e32 %[sub], %[ck], %[cm], vcc\n\t"                  \
-    "v_mov_b32_dpp %[sh], %[G] wave_shr:1 row_mask:0xf bank_mask:0xf\n\t" \
-    "v_subrev_u32_e32 %[lf], %[d], %[G]\n\t"                           \
-    "v_add_u32_e32 %[dg], %[sh], %[sub]\n\t"                           \
-    "v_max3_i32 %[Y], %[lf], %[dg], %[top]\n\t"
-#define NW_DPP(CTRL) "v_max_i32_dpp %[Y], %[Y], %[Y] " CTRL "\n\t"
-#define NW_FILL_A                                                      \
-    "v_cmp_eq_i32_e64 %[sa], %[pG], %[pdg]\n\t"                        \
-    "v_cmp_eq_i32_e64 %[sb], %[pG], %[sh]\n\t"
-#define NW_FILL_B                                                      \
-    "v_cmp_eq_i32_e32 vcc, %[pG], %[plf]\n\t"                          \
-    "v_lshlrev_b32_e32 %[acc], 1, %[acc]\n\t"
-#define NW_FILL_C                                                      \
-    "v_addc_co_u32_e64 %[acc], %[junk], %[acc], %[acc], vcc\n\t"       \
-    "v_addc_co_u32_e64 %[acc], %[junk], %[acc], %[acc], %[sb]\n\t"
-#define NW_FILL_D                                                      \
-    "v_addc_co_u32_e64 %[acc], %[junk], %[acc], %[acc], %[sa]\n\t"     \
-    "v_sub_u32_e32 %[Hp], %[pG], %[lo]\n\t"
-#define NW_FILL_E                                                      \
-    "v_sub_u32_e32 %[tmp], 0, %[Hp]\n\t"                               \
-    "v_max3_i32 %[gav], %[gav], %[Hp], %[tmp]\n\t"
-#define NW_NOP2 "s_nop 1\n\t"
-#define NW_SCAN_FILLED(E)                                              \
-    NW_FILL_A NW_DPP("row_shr:1 row_mask:0xf bank_mask:0xf")           \
-    NW_FILL_B NW_DPP("row_shr:2 row_mask:0xf bank_mask:0xf")           \
-    NW_FILL_C NW_DPP("row_shr:4 row_mask:0xf bank_mask:0xf")           \
-    NW_FILL_D NW_DPP("row_shr:8 row_mask:0xf bank_mask:0xf")           \
-    E         NW_DPP("row_bcast:15 row_mask:0xa bank_mask:0xf")        \
-    NW_NOP2   "v_max_i32_dpp %[Y], %[Y], %[Y] row_bcast:31 row_mask:0xc bank_mask:0xf"
-#define NW_SCAN_BARE                                                   \
-    NW_NOP2 NW_DPP("row_shr:1 row_mask:0xf bank_mask:0xf")             \
-    NW_NOP2 NW_DPP("row_shr:2 row_mask:0xf bank_mask:0xf")             \
-    NW_NOP2 NW_DPP("row_shr:4 row_mask:0xf bank_mask:0xf")             \
-    NW_NOP2 NW_DPP("row_shr:8 row_mask:0xf bank_mask:0xf")             \
-    NW_NOP2 NW_DPP("row_bcast:15 row_mask:0xa bank_mask:0xf")          \
-    NW_NOP2 "v_max_i32_dpp %[Y], %[Y], %[Y] row_bcast:31 row_mask:0xc bank_mask:0xf"
+constexpr int SUPER_CHUNKS = 512;     // chunks per super-chunk (4096 columns)
 
-struct StepIO {
-    int G, sh, dg, lf;      // this step: new G (out), shift / diag / left candidates
-    int pG, pdg, plf;       // previous step (inputs of the filled outputs)
-    int Hp;                 // previous step's score (out)
-    uint32_t acc;           // direction codes accumulator
-    int gav;                // running max |H|
+__device__ __forceinline__ int chunk_base(int c) { return (c / SUPER_CHUNKS) * (SUPER_CHUNKS * CH); }
+
+struct ChunkRegs {
+    int g[6];           // out: G' after steps 0..5 (lane 63 -> the wave below)
+    int gp6, gin;       // in: G' of the previous chunk's columns 7, 8; out: this chunk's
+    int t[8];           // in: T' of each step (t[s-1] is reused for wave_shr1 of step s)
+    int tm;             // in: T' of the previous column; out: T' of this chunk's last
+    int dgA, dgB;       // diagonal candidates of even / odd steps (dgB: last step of a full chunk)
+    int subA, subB;     // sub' of even / odd steps (subA: step 0 of the next chunk)
+    int h[8];           // out: H of steps 0..7 (partial chunks: the flush block adds the last)
+    uint32_t accp;      // in: previous chunk's codes (missing the last); out: this chunk's so far
+    uint32_t acc;       // out: previous chunk's complete codes word
+    int gav;            // in/out: running max |H| (stats)
+};
+struct ChunkConst {
+    uint32_t c2;        // this lane's side-string byte
+    int vcm, vck;       // sub' for match / mismatch
+    int nlo;            // -(r*d) - (8c - base)*d: H = G' + nlo - (s+1)*d
+    int kd[8];          // -(s+1)*d
+    int hv;             // lane*4: byte offset of this lane in a score-tile column
+};
+struct ChunkChars {
+    uint32_t lo, hi;    // this chunk's 8 top-string bytes
+    uint32_t nlo;       // next chunk's first 4 bytes
 };
 
-// MODE 0: first step of a chunk (nothing pending), 1: fill with the previous
-// step's code + score, 2: also its |H| for the stats.
-template <int MODE>
-__device__ __forceinline__ void step_asm(StepIO& io, int Tprev, int top, uint32_t ch, uint32_t c2, int vck, int vcm,
-                                         int d, int laneoff) {
-    int Y, sub, tmp;
-    uint64_t sa, sb, junk;
-    int sh = Tprev;  // DPP lane 0 keeps the old value: the row above
-#define NW_OPERANDS                                                                              \
-    : [Y] "=&v"(Y), [sh] "+v"(sh), [sub] "=&v"(sub), [dg] "=&v"(io.dg), [lf] "=&v"(io.lf),        \
-      [Hp] "=&v"(io.Hp), [acc] "+v"(io.acc), [gav] "+v"(io.gav), [tmp] "=&v"(tmp), [sa] "=&s"(sa), \
-      [sb] "=&s"(sb), [junk] "=&s"(junk)                                                          \
-    : [G] "v"(io.G), [ch] "s"(ch), [c2] "v"(c2), [ck] "v"(vck), [cm] "v"(vcm), [d] "s"(d),       \
-      [top] "v"(top), [pG] "v"(io.pG), [pdg] "v"(io.pdg), [plf] "v"(io.plf), [lo] "v"(laneoff)    \
-    : "vcc"
-    if constexpr (MODE == 0) {
-        asm volatile(NW_STEP_HEAD NW_SCAN_BARE NW_OPERANDS);
-    } else if constexpr (MODE == 1) {
-        asm volatile(NW_STEP_HEAD NW_SCAN_FILLED(NW_NOP2) NW_OPERANDS);
-    } else {
-        asm volatile(NW_STEP_HEAD NW_SCAN_FILLED(NW_FILL_E) NW_OPERANDS);
-    }
-#undef NW_OPERANDS
-    io.sh = sh;
-    io.G = Y;
+#include "nw_chunk.inc"
+
+// Count 3-bit codes of a word (8 per word, bits 0..23) with >= 2 directions.
+__device__ __forceinline__ uint32_t branch_codes(uint32_t x) {
+    const uint32_t y = (x & (x >> 1)) | (x & (x >> 2)) | ((x >> 1) & (x >> 2));
+    return __builtin_popcount(y & 0x249249u);
 }
 
-// One 8-column chunk of one wave.  NSTEP is 8 except for the last chunk.
-// Cell recurrence = needleman-wunsch.c:429-465; direction flags :485-503.
-// In the shifted domain G = H + r*d each column is a prefix max over lanes:
-//     G_i = prefmax( max(G_{i-1} - d, G_{i-1}[l-1] + sub_i, T_i) ).
-template <bool SH, bool SD, bool ST, bool LAST>
-__device__ __forceinline__ void chunk_body(const FillArgs& a, WaveState& st, const int* T, uint64_t ch8, int c,
-                                           int nstep, int lane, int64_t tile_off, int j0, int d, int vcm, int vck,
-                                           int* bot_wr, uint32_t* dword_out) {
-    // Buffer descriptor on this chunk's two column quads (2 KB contiguous in
-    // the stripe-major quad layout): lane l stores its 4 consecutive columns
-    // as one 16-byte buffer_store_dwordx4 at lane*16 (+1024 for the 2nd quad).
-    int32_t* cb = a.H + tile_off + (int64_t)c * 512;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(cb, 0, 0x7fffffff, 0x00020000);
-    StepIO io;
-    io.G = st.G;
-    io.acc = 0;
-    io.gav = st.gav;
-    io.pG = io.pdg = io.plf = 0;
-    int Tprev = st.Tprev;
-    int h[CH];
-#pragma unroll
-    for (int s = 0; s < CH; ++s) {
-        if (LAST && s >= nstep) break;
-        const uint32_t ch = (uint32_t)(ch8 >> (8 * s)) & 0xffu;
-        if (s == 0) step_asm<0>(io, Tprev, T[s], ch, st.c2, vck, vcm, d, st.laneoff);
-        else if (ST) step_asm<2>(io, Tprev, T[s], ch, st.c2, vck, vcm, d, st.laneoff);
-        else step_asm<1>(io, Tprev, T[s], ch, st.c2, vck, vcm, d, st.laneoff);
-        if (s > 0) h[s - 1] = io.Hp;
-        if (SH && !LAST && s == 4)
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4(h[0], h[1], h[2], h[3]), rs, lane * 16, 0, 0);
-        bot_wr[s] = io.G;   // lane 63 -> bottom-row slot, lanes 0..62 -> scratch
-        io.pG = io.G;
-        io.pdg = io.dg;
-        io.plf = io.lf;
-        Tprev = T[s];
+// The last chunk of a stripe (n = 1..8 columns): block + flush.
+// G' of step s of the current chunk (steps 6, 7 live in the carried registers).
+__device__ __forceinline__ int g_of(const ChunkRegs& r, int s) {
+    switch (s) {
+        case 0: return r.g[0];
+        case 1: return r.g[1];
+        case 2: return r.g[2];
+        case 3: return r.g[3];
+        case 4: return r.g[4];
+        case 5: return r.g[5];
+        case 6: return r.gp6;
+        default: return r.gin;
     }
-    // Outputs of the chunk's last step (not overlapped).
-    const int slast = LAST ? nstep - 1 : CH - 1;
-    const int up = wave_shr1(Tprev, io.G);
-    const int Hv = io.G - st.laneoff;
-    h[slast] = Hv;
-    if (SH) {
-        if (LAST) {
-            // partial chunk: unused slots land in the quad padding
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4(h[0], nstep > 1 ? h[1] : 0, nstep > 2 ? h[2] : 0,
-                                                             nstep > 3 ? h[3] : 0), rs, lane * 16, 0, 0);
-            if (nstep > 4)
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4(h[4], nstep > 5 ? h[5] : 0, nstep > 6 ? h[6] : 0,
-                                                                 nstep > 7 ? h[7] : 0), rs, lane * 16 + 1024, 0, 0);
-        } else {
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4(h[4], h[5], h[6], h[7]), rs, lane * 16 + 1024, 0, 0);
-        }
+}
+
+// Returns H of the stripe's last column (for the score-only last column).
+template <bool SH, bool SD, bool ST, int N>
+__device__ __forceinline__ int run_last(ChunkRegs& r, const ChunkConst& k, const ChunkChars& ch, int ra,
+                                        const int32_t* hb) {
+    chunk_asm<SH, SD, ST, N, false>(r, k, ch, ra, hb);
+    flush_asm<SH, SD, ST, N>(r, k, ra, hb);
+    if constexpr (SH || ST) return r.h[N - 1];
+    else return g_of(r, N - 1) + k.nlo + k.kd[N - 1];
+}
+template <bool SH, bool SD, bool ST>
+__device__ __forceinline__ int run_last_n(int n, ChunkRegs& r, const ChunkConst& k, const ChunkChars& ch, int ra,
+                                          const int32_t* hb) {
+    switch (n) {
+        case 1: return run_last<SH, SD, ST, 1>(r, k, ch, ra, hb);
+        case 2: return run_last<SH, SD, ST, 2>(r, k, ch, ra, hb);
+        case 3: return run_last<SH, SD, ST, 3>(r, k, ch, ra, hb);
+        case 4: return run_last<SH, SD, ST, 4>(r, k, ch, ra, hb);
+        case 5: return run_last<SH, SD, ST, 5>(r, k, ch, ra, hb);
+        case 6: return run_last<SH, SD, ST, 6>(r, k, ch, ra, hb);
+        case 7: return run_last<SH, SD, ST, 7>(r, k, ch, ra, hb);
+        default: return run_last<SH, SD, ST, 8>(r, k, ch, ra, hb);
     }
-    uint32_t acc = (io.acc << 4) | (uint32_t)(io.G == io.dg) | ((uint32_t)(io.G == up) << 1) |
-                   ((uint32_t)(io.G == io.lf) << 2);
-    if (ST) io.gav = max(io.gav, iabs(Hv));
-    if (LAST && !SH) a.lastcol[j0 + lane] = Hv;            // score-only: H[L1][*]
-    if (LAST && nstep < CH) acc <<= 4 * (CH - nstep);
-    st.G = io.G;
-    st.Tprev = Tprev;
-    st.gav = io.gav;
-    *dword_out = acc;
 }
 
 // Hand-off granule load: agent scope between workgroups of one fill, system
@@ -272,9 +187,9 @@ __device__ __forceinline__ int lds_ld(const int* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void lds_publish(int* p, int v) {
-    // Every LDS write this wave issued before (ring data) completes first:
-    // LDS is in-order per wave, and the wait makes the counter the last word.
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // Every LDS write this wave issued before (ring data) lands first: the
+    // LDS executes one wave's DS instructions in order, so a reader that sees
+    // the counter and then reads the ring sees the data.
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -286,12 +201,14 @@ __device__ __forceinline__ void lds_publish(int* p, int v) {
 // has taken out of it; a producer only waits when it is R chunks ahead.
 // The loader feeds tring[0] from the previous WG-stripe's granules; it issues
 // no stores, so its waits on the hand-off loads are exact, and the compute
-// waves never wait on vmcnt.
+// waves never wait on vmcnt.  Granules (between workgroups and panels) carry
+// H - d of the row above in the plain domain; ring slots carry G'.
 template <int W, bool SH, bool SD, bool ST>
 __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
     constexpr int R = 4;
+    constexpr bool F = SD || ST;     // direction codes
     __shared__ __attribute__((aligned(16))) int tring[(W + 1) * R * CH];
-    __shared__ int scratch[64 + CH];
+    __shared__ __attribute__((aligned(16))) int scratch[64 * CH + R * CH];   // ring writes of lanes 0..62
     __shared__ int prog[W + 1];
     __shared__ int cons[W + 1];
     __shared__ int sh_sidx;
@@ -301,9 +218,8 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
     const int w = uni(threadIdx.x >> 6);
     const bool loader = (w == W);
     const int d = a.d;
-    int vcm = a.m + a.d;
-    int vck = a.d - a.k;
-    asm volatile("" : "+v"(vcm), "+v"(vck));   // keep both as VGPR operands of v_cndmask
+    int vcm = a.m + 2 * a.d;
+    int vck = 2 * a.d - a.k;
     const int NC = a.NC;
     const int nlast = a.L1 - CH * (NC - 1);   // steps in the last chunk (1..8)
 
@@ -329,10 +245,8 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
         const bool next_real = !loader && w + 1 < W && g + 1 < a.NG;
         const int j0 = 1 + 64 * g;                 // first row of the wave stripe
         const int jrow = j0 + lane;
-        WaveState st;
-        st.G = 0;
-        st.gav = 0;
-        st.bc = 0;
+        int gav = 0;
+        uint32_t bc = 0;
 
         if (loader) {
             // ---------------- loader wave: no stores, exact waits ----------------
@@ -349,9 +263,10 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
                 const int n = (c == NC - 1) ? nlast : CH;
                 while (lds_ld(&cons[0]) < c - R + 1) __builtin_amdgcn_s_sleep(1);   // ring slot free?
                 int* dst = &tring[(c % R) * CH];
+                const int base = chunk_base(c);
                 if (seeded) {
-                    // row 0: H[i][0] - d = -(i+1)*d   (computation.c:102-110)
-                    if (lane < CH) dst[lane] = -(CH * c + 2 + lane) * d;
+                    // row 0: H[i][0] - d = -(i+1)*d (computation.c:102-110) -> G' = -(base+1)*d
+                    if (lane < CH) dst[lane] = -(base + 1) * d;
                 } else {
                     bool ok = lane >= n || (uint32_t)(pf >> 32) == want;
                     if (!__all(ok)) {
@@ -380,7 +295,8 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
                         }
                     }
                     if (lds_ld(&sh_abort)) break;
-                    if (lane < CH) dst[lane] = (int)(uint32_t)pf;
+                    // H - d of the row above -> G' of lane -1: + (i - base)*d
+                    if (lane < CH) dst[lane] = (int)(uint32_t)pf + (CH * c + lane + 1 - base) * d;
                     if (c + 1 < NC && lane < CH)          // prefetch the next chunk
                         pf = ld_gran(gin + CH * (int64_t)(c + 1) + lane, xsrc);
                 }
@@ -389,17 +305,49 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
         } else if (real) {
             // ---------------- compute wave: its 64-row stripe, chunk by chunk ----
             uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
-            const int64_t tile_off = (int64_t)g * a.spitch;
-            st.c2 = a.s2[jrow - 1];
-            st.laneoff = (64 * w + lane) * d;
-            // column 0: H[0][j] = -j*d  ->  G = -(1 + row_base + 64*sidx*W)*d for every lane.
-            st.G = -(1 + a.row_base + 64 * sidx * W) * d;
-            st.Tprev = st.G;
+            int32_t* tile = a.H + (int64_t)g * a.spitch;
             const bool publish = (w == W - 1) && sidx + 1 < a.NSW;
             // The wave holding the panel's last row (lane 63: panels above the
             // last one have a multiple of 64 rows) feeds the panel below.
             const bool xpublish = a.xout && g == a.NG - 1;
+            const bool out_lane = jrow <= a.L2;
             const int* tin = &tring[w * R * CH];
+            int* tout = &tring[(w + 1) * R * CH];
+            ChunkConst kc;
+            kc.c2 = a.s2[jrow - 1];
+            asm volatile("" : "+v"(vcm), "+v"(vck));   // VGPR operands of v_cndmask
+            kc.vcm = vcm;
+            kc.vck = vck;
+            kc.nlo = -(64 * w + lane) * d;
+            kc.hv = lane * 4;
+#pragma unroll
+            for (int s = 0; s < CH; ++s) {
+                kc.kd[s] = -(s + 1) * d;
+                asm volatile("" : "+v"(kc.kd[s]));     // keep the constants in VGPRs
+            }
+            ChunkRegs r;
+            // column 0: H[0][j] = -j*d (computation.c:112-120) -> G' = -(1 + row_base + 64*sidx*W)*d
+            r.gin = -(1 + a.row_base + 64 * sidx * W) * d;
+            r.gp6 = r.gin;
+            r.tm = r.gin;
+            r.dgA = r.dgB = 0;
+            r.accp = 0;
+            r.gav = 0;
+            r.subA = ((uint32_t)a.s1[0] == kc.c2) ? vcm : vck;
+            r.subB = 0;
+            // Ring writes: lane 63 into the slot, the other lanes into a
+            // per-lane dummy, so no exec juggling per chunk.  One address per
+            // ring slot (the chunk loop is unrolled by R).
+            const int ring0 = lane == 63 ? lds_addr(tout) : lds_addr(&scratch[lane * CH]);
+            int ra[R];
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                ra[q] = ring0 + q * CH * 4;
+                asm volatile("" : "+v"(ra[q]));
+            }
+            const int32_t* hb = tile;                   // score tile of the current chunk
+            uint32_t* dchunk = a.D + (int64_t)g * NC * 64;      // codes of the previous chunk (c - 1)
+            const uint8_t* s1c = a.s1;                  // top-string bytes of chunk c
             if (a.trace && lane == 0 && w == 0) a.trace[4 * (int64_t)sidx + 1] = __builtin_amdgcn_s_memrealtime();
             // Chunk prologue, software-pipelined one chunk ahead: the s1 bytes
             // (s_load), our producer's progress, the ring slot and our
@@ -409,64 +357,60 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             // valid.  (s_load shares lgkmcnt with LDS, so it is issued first.)
             uint64_t ch8 = *(cptr64)(a.s1);
             int pin = lds_ld(&prog[w]);
-            int4 t03 = *reinterpret_cast<const int4*>(&tin[0]);
-            int4 t47 = *reinterpret_cast<const int4*>(&tin[4]);
+            int tA[CH], tB[CH];
+#pragma unroll
+            for (int s = 0; s < CH; ++s) tA[s] = tin[s];
             int pout = next_real ? lds_ld(&cons[w + 1]) : (1 << 30);
-            for (int c = 0; c < NC; ++c) {
-                const int slot = (c % R) * CH;
-                if (pin <= c || pout < c - R + 1) {
-                    // slow path: producer behind (or ring full) -- wait, then re-read
-                    for (;;) {
-                        pin = lds_ld(&prog[w]);
-                        pout = next_real ? lds_ld(&cons[w + 1]) : (1 << 30);
-                        if ((pin > c && pout >= c - R + 1) || lds_ld(&sh_abort)) break;
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                    if (lds_ld(&sh_abort)) break;
-                    t03 = *reinterpret_cast<const int4*>(&tin[slot]);
-                    t47 = *reinterpret_cast<const int4*>(&tin[slot + 4]);
-                }
-                const int T[CH] = {t03.x, t03.y, t03.z, t03.w, t47.x, t47.y, t47.z, t47.w};
-                const uint64_t ch8c = ch8;
-                if (lane == 0) __hip_atomic_store(&cons[w], c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (c + 1 < NC) {
-                    const int nslot = ((c + 1) % R) * CH;
-                    ch8 = *(cptr64)(a.s1 + 8 * (int64_t)(c + 1));
+            bool aborted = false;
+            // Wait until chunk c's ring slot is filled (and our consumer has
+            // room), re-reading the slot if the prefetch was too early.
+            auto wait_slot = [&](int c, int slot, int (&tt)[CH]) -> bool {
+                if (pin > c && pout >= c - R + 1) return true;
+                for (;;) {
                     pin = lds_ld(&prog[w]);
-                    t03 = *reinterpret_cast<const int4*>(&tin[nslot]);
-                    t47 = *reinterpret_cast<const int4*>(&tin[nslot + 4]);
-                    if (next_real) pout = lds_ld(&cons[w + 1]);
+                    pout = next_real ? lds_ld(&cons[w + 1]) : (1 << 30);
+                    if ((pin > c && pout >= c - R + 1) || lds_ld(&sh_abort)) break;
+                    __builtin_amdgcn_s_sleep(1);
                 }
-                int* bot_wr = (lane == 63) ? &tring[(w + 1) * R * CH + slot] : &scratch[lane];
-                const int nstep = (c == NC - 1) ? nlast : CH;
-                uint32_t dw;
-                if (c == NC - 1)
-                    chunk_body<SH, SD, ST, true>(a, st, T, ch8c, c, nstep, lane, tile_off, j0, d, vcm, vck, bot_wr, &dw);
-                else
-                    chunk_body<SH, SD, ST, false>(a, st, T, ch8c, c, CH, lane, tile_off, j0, d, vcm, vck, bot_wr, &dw);
-                if (next_real && lane == 0) lds_publish(&prog[w + 1], c + 1);
-                if (jrow > a.L2) dw = 0;
-                if (SD) a.D[((int64_t)g * NC + c) * 64 + lane] = dw;
-                if (ST) st.bc += branch_nibbles(dw);
-                // Last wave of a non-final WG-stripe publishes its bottom row.
-                if (publish) {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    if (lane < nstep) {
-                        const int v = tring[W * R * CH + slot + lane] - 64 * W * d;  // row-above domain
-                        const uint64_t gr = ((uint64_t)(uint32_t)(sidx + 1) << 32) | (uint32_t)v;
-                        __hip_atomic_store(gout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+                if (lds_ld(&sh_abort)) return false;
+#pragma unroll
+                for (int s = 0; s < CH; ++s) tt[s] = tin[slot + s];
+                return true;
+            };
+            // After chunk c's block: hand the ring slot to the wave below,
+            // store the previous chunk's codes, publish the WG-stripe's bottom
+            // row (last wave) and advance the per-chunk pointers.
+            auto after_chunk = [&](int c, int slot, int n, bool last) {
+                if (next_real) lds_publish(&prog[w + 1], c + 1);
+                if (F) {
+                    // codes trail by one column: the previous chunk's word completes now
+                    if (c > 0) {
+                        const uint32_t dw = out_lane ? r.acc : 0u;
+                        if (SD) dchunk[lane] = dw;
+                        if (ST) bc += branch_codes(dw);
+                        dchunk += 64;
+                    }
+                    if (last) {
+                        const uint32_t dw = out_lane ? (r.accp << (3 * (CH - n))) : 0u;
+                        if (SD) dchunk[lane] = dw;
+                        if (ST) bc += branch_codes(dw);
                     }
                 }
-                if (xpublish) {
+                // (plain domain: H - d = G' - 64(w+1)d - (i - base)d)
+                if (publish || xpublish) {
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    if (lane < nstep) {
-                        const int v = tring[(w + 1) * R * CH + slot + lane] - 64 * (w + 1) * d;
-                        const uint64_t gr = ((uint64_t)a.epoch << 32) | (uint32_t)v;
-                        __hip_atomic_store(a.xout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (lane < n) {
+                        const int v = tout[slot + lane] - 64 * (w + 1) * d - (CH * c + lane + 1 - chunk_base(c)) * d;
+                        const uint64_t tag = publish ? (uint32_t)(sidx + 1) : a.epoch;
+                        const uint64_t gr = (tag << 32) | (uint32_t)v;
+                        if (publish)
+                            __hip_atomic_store(gout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        else
+                            __hip_atomic_store(a.xout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
                     }
-                    if (a.xflag && ((c + 1) % a.xblk == 0 || c == NC - 1)) {
+                    if (xpublish && a.xflag && ((c + 1) % a.xblk == 0 || last)) {
                         // block complete: its granules are out before the flag
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         if (lane == 0)
@@ -474,13 +418,95 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
                                                __HIP_MEMORY_SCOPE_SYSTEM);
                     }
                 }
+                kc.nlo -= CH * d;
+                hb += CH * 64;
+                s1c += CH;
+            };
+            // One full (non-final) chunk; SLOT = c % R is a compile-time ring slot.
+            auto full_chunk = [&](int c, auto slotc, int (&cur)[CH], int (&nxt)[CH]) -> bool {
+                constexpr int SLOT = decltype(slotc)::value;
+                constexpr int NSLOT = ((SLOT + 1) % R) * CH;
+                if (!wait_slot(c, SLOT * CH, cur)) return false;
+#pragma unroll
+                for (int s = 0; s < CH; ++s) r.t[s] = cur[s];
+                const uint64_t ch8c = ch8;
+                // ring slot consumed (every lane stores the same word: no exec mask)
+                __hip_atomic_store(&cons[w], c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                ch8 = *(cptr64)(s1c + CH);
+                pin = lds_ld(&prog[w]);
+#pragma unroll
+                for (int s = 0; s < CH; ++s) nxt[s] = tin[NSLOT + s];
+                if (next_real) pout = lds_ld(&cons[w + 1]);
+                const ChunkChars chs{(uint32_t)ch8c, (uint32_t)(ch8c >> 32), (uint32_t)ch8};
+                chunk_asm<SH, SD, ST, 8, true>(r, kc, chs, ra[SLOT], hb);
+                after_chunk(c, SLOT * CH, CH, false);
+                return true;
+            };
+            using S0 = std::integral_constant<int, 0>;
+            using S1 = std::integral_constant<int, 1>;
+            using S2 = std::integral_constant<int, 2>;
+            using S3 = std::integral_constant<int, 3>;
+            int c = 0;
+            const int nfull = NC - 1;              // chunks before the last one
+            while (c + R <= nfull && !aborted) {
+                if (c > 0 && c % SUPER_CHUNKS == 0) {
+                    // new super-chunk: rebase the carried G' values (and nlo)
+                    const int sh = SUPER_CHUNKS * CH * d;
+                    r.gin -= sh;
+                    r.gp6 -= sh;
+                    r.dgB -= sh;
+                    r.tm -= sh;
+                    kc.nlo += sh;
+                }
+                aborted = !full_chunk(c, S0{}, tA, tB) || !full_chunk(c + 1, S1{}, tB, tA) ||
+                          !full_chunk(c + 2, S2{}, tA, tB) || !full_chunk(c + 3, S3{}, tB, tA);
+                c += R;
             }
+            if (!aborted && c < nfull) {
+                if (c > 0 && c % SUPER_CHUNKS == 0) {
+                    const int sh = SUPER_CHUNKS * CH * d;
+                    r.gin -= sh;
+                    r.gp6 -= sh;
+                    r.dgB -= sh;
+                    r.tm -= sh;
+                    kc.nlo += sh;
+                }
+                aborted = !full_chunk(c, S0{}, tA, tB);
+                if (!aborted && c + 1 < nfull) aborted = !full_chunk(c + 1, S1{}, tB, tA);
+                if (!aborted && c + 2 < nfull) aborted = !full_chunk(c + 2, S2{}, tA, tB);
+                c = nfull;
+            }
+            if (!aborted) {
+                // the last chunk (n = 1..8 columns), ring slot known only at run time
+                const int slot = (c % R) * CH;
+                pin = -1;                                   // force a (re-)read of the slot
+                if (wait_slot(c, slot, tA)) {
+                    if (c > 0 && c % SUPER_CHUNKS == 0) {
+                        const int sh = SUPER_CHUNKS * CH * d;
+                        r.gin -= sh;
+                        r.gp6 -= sh;
+                        r.dgB -= sh;
+                        r.tm -= sh;
+                        kc.nlo += sh;
+                    }
+#pragma unroll
+                    for (int s = 0; s < CH; ++s) r.t[s] = tA[s];
+                    __hip_atomic_store(&cons[w], c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const ChunkChars chs{(uint32_t)ch8, (uint32_t)(ch8 >> 32), 0u};
+                    const int n = nlast;
+                    const int rs = ring0 + slot * 4;
+                    const int hl = run_last_n<SH, SD, ST>(n, r, kc, chs, rs, hb);
+                    if (!SH) a.lastcol[j0 + lane] = hl;   // score-only: H[L1][*]
+                    after_chunk(c, slot, n, true);
+                }
+            }
+            gav = r.gav;
         }
         if (a.trace && threadIdx.x == 64 * (W - 1)) a.trace[4 * (int64_t)sidx + 2] = __builtin_amdgcn_s_memrealtime();
         if (ST && real) {
             const bool rowok = jrow <= a.L2;
-            int gv = rowok ? st.gav : 0;
-            uint32_t bv = rowok ? st.bc : 0u;
+            int gv = rowok ? gav : 0;
+            uint32_t bv = rowok ? bc : 0u;
             for (int o = 32; o > 0; o >>= 1) {
                 gv = max(gv, __shfl_xor(gv, o));
                 bv += __shfl_xor(bv, o);
@@ -516,16 +542,16 @@ struct TableView {
 // Score of cell (i, j) in the device layout.  Row 0 and column 0 are the
 // reference's seeds (computation.c:93-120), computed, not stored; a panel's
 // row 0 is the last row of the panel above, kept in its xin granules.
-// Interior cells live in stripe-major quad tiles: stripe g = (j-1)/64, lane
-// l = (j-1)%64, column quad q = (i-1)/4, r = (i-1)%4 at
-//     g*spitch + (q*64 + l)*4 + r,   spitch = 512*NC,
-// i.e. each lane's 4 consecutive columns are one 16-byte word and one quad of
-// one stripe is 1 KB contiguous.
+// Interior cells live in column-major stripe tiles: stripe g = (j-1)/64,
+// lane l = (j-1)%64, column i at
+//     g*spitch + (i-1)*64 + l,   spitch = 512*NC,
+// i.e. one column of one stripe is 256 contiguous bytes (one coalesced
+// store per column step of the fill).
 __device__ __forceinline__ int32_t score_at(const TableView& v, int64_t i, int64_t j) {
     if (i == 0) return (int32_t)(-(j + v.row_base) * (int64_t)v.d);
     if (j == 0) return v.top ? (int32_t)(uint32_t)v.top[i - 1] + v.d : (int32_t)(-i * (int64_t)v.d);
     const int64_t r = j - 1, c = i - 1;
-    return v.tiles[(r >> 6) * v.spitch + (((c >> 2) * 64 + (r & 63)) << 2) + (c & 3)];
+    return v.tiles[(r >> 6) * v.spitch + c * 64 + (r & 63)];
 }
 
 // Dense i-major copy of columns [i0, i1): out[(i-i0)*(L2+1) + j].
@@ -544,7 +570,7 @@ __device__ __forceinline__ uint32_t code_at(const TableView& v, int64_t i, int64
     if (i == 0) return j == 0 ? 0u : 2u;          // (0,0): none; (0,j): up
     if (j == 0) return 4u;                         // (i,0): left
     const int64_t g = (j - 1) >> 6, l = (j - 1) & 63, q = (i - 1) >> 3, s = (i - 1) & 7;
-    return (v.D[(g * v.NC + q) * 64 + l] >> (28 - 4 * s)) & 0xfu;
+    return (v.D[(g * v.NC + q) * 64 + l] >> (21 - 3 * s)) & 7u;
 }
 
 // Dense nibble packing for nw_fill(): byte b = code(2b) | code(2b+1) << 4.
@@ -656,12 +682,13 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
     if (t->launched) return fail(NW_ERR_STATE, "nw_table_fill: a fill is already in flight");
     if ((out_mask & ~t->cap_mask & (NW_OUT_SCORES | NW_OUT_DIRS)) != 0)
         return fail(NW_ERR_ARG, "nw_table_fill: output not allocated at creation");
-    // Overflow guard: |H| <= (L1+L2)*max(|m|,|k|,|d|); the shifted domain
-    // adds up to 64*W*|d| (W <= 16) and one more candidate term.
+    // Overflow guard: |H| <= (L1+L2)*max(|m|,|k|,|d|); the kernel's shifted
+    // domain adds r*d + (i - base)*d <= (64*16 + 4096 + 8)*|d| and one more
+    // candidate term (sub' = m + 2d or 2d - k).
     {
         const int64_t M = std::max({std::llabs(m), std::llabs(k), std::llabs(d)});
         const int64_t L2g = t->L2_total >= 0 ? t->L2_total : t->L2;
-        const int64_t bound = (t->L1 + L2g) * M + 1024 * std::llabs(d) + 2 * M + 2;
+        const int64_t bound = (t->L1 + L2g) * M + 6144 * std::llabs(d) + 4 * M + 2;
         if (bound >= (int64_t)INT32_MAX)
             return fail(NW_ERR_RANGE, "nw_table_fill: |scores| could reach " + std::to_string(bound));
     }
@@ -764,8 +791,7 @@ int fill_finish(nw_table* t) {
     int32_t corner = 0;
     if (L1 > 0 && L2 > 0) {
         const int64_t r = L2 - 1, q = L1 - 1;
-        const int32_t* src = sh ? t->H + (r >> 6) * t->spitch + (((q >> 2) * 64 + (r & 63)) << 2) + (q & 3)
-                                : t->lastcol + L2;
+        const int32_t* src = sh ? t->H + (r >> 6) * t->spitch + q * 64 + (r & 63) : t->lastcol + L2;
         NW_HIPCHK(hipMemcpyAsync(&corner, src, 4, hipMemcpyDeviceToHost, t->stream));
     }
     NW_HIPCHK(hipStreamSynchronize(t->stream));
