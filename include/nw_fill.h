@@ -136,10 +136,11 @@ int nw_table_copy_codes(nw_table *t, int64_t i0, int64_t i1, uint8_t *dst);
 int nw_table_copy_last_column(nw_table *t, int32_t *dst);
 /* Geometry of the device layout (for zero-copy consumers). */
 int64_t nw_table_score_pitch(const nw_table *t);
-/* In-kernel timeline of the last fill, recorded only when $NW_TRACE is set
- * (s_memrealtime, 100 MHz): 4 words per workgroup stripe s -- [4s] dequeued,
- * [4s+1] first chunk started, [4s+2] last wave finished, [4s+3] blockIdx |
- * hardware CU id << 32.  Copies min(n, total) words into dst (if non-NULL)
+/* In-kernel timeline of the last fill, recorded only when $NW_TRACE is set:
+ * 8 words per workgroup stripe s -- s_memrealtime (100 MHz) at [8s] dequeue,
+ * [8s+1] first wave started, [8s+2] last wave finished; [8s+3] blockIdx |
+ * hardware CU id << 32; s_memtime (shader clock) at [8s+4] first wave
+ * started, [8s+5] last wave finished; [8s+6..7] reserved.  Copies min(n, total) words into dst (if non-NULL)
  * and returns the total word count (0 when no trace was recorded). */
 int64_t nw_table_trace(nw_table *t, uint64_t *dst, int64_t n);
 /* Waves per workgroup chosen for the last fill (tuning / reporting). */

@@ -57,7 +57,9 @@ struct FillArgs {
     int32_t m, k, d;
     int32_t NC;             // chunks = ceil(L1 / 8)
     int32_t NG;             // wave stripes = ceil(L2 / 64)
-    int32_t NSW;            // workgroup stripes = ceil(NG / W)
+    int32_t NSW;            // workgroup stripes (WG-stripes)
+    int32_t SQ, SR;         // WG-stripe k holds stripes g0 = k*SQ + min(k, SR) .. + SQ + (k < SR) - 1
+                            // (clipped to NG): the first SR WG-stripes hold one stripe more
     int32_t* H;             // score tiles, see score_at()
     int64_t spitch;         // 512*NC: elements per 64-row stripe
     uint32_t* D;            // codes: word ((g*NC + q)*64 + lane)
@@ -66,7 +68,7 @@ struct FillArgs {
     int64_t gpitch;
     int32_t nslot;
     uint32_t* ctl;          // CtlWord
-    uint64_t* trace;        // optional timeline: 4 words per WG-stripe (see nw_table_trace)
+    uint64_t* trace;        // optional timeline: 8 words per WG-stripe (see nw_table_trace)
     int64_t spin_ticks;     // hand-off watchdog (s_memrealtime ticks)
     // Row panels (multi-GPU, nw_panel.h).  The table holds global rows
     // row_base+1 .. row_base+L2; row 0 is the boundary row of the panel above.
@@ -208,7 +210,10 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
     constexpr int R = 4;
     constexpr bool F = SD || ST;     // direction codes
     __shared__ __attribute__((aligned(16))) int tring[(W + 1) * R * CH];
-    __shared__ __attribute__((aligned(16))) int scratch[64 * CH + R * CH];   // ring writes of lanes 0..62
+    // Dummy target of the ring writes of lanes 0..62: lane-contiguous, so a
+    // ds_write_b32 of the whole wave is bank-conflict free (an 8-dword lane
+    // stride made every ring write a 16-way conflict).
+    __shared__ int scratch[64 + R * CH + CH];
     __shared__ int prog[W + 1];
     __shared__ int cons[W + 1];
     __shared__ int sh_sidx;
@@ -236,13 +241,15 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
         const int sidx = uni(sh_sidx);
         if (sidx >= a.NSW || sh_abort) break;
         if (a.trace && threadIdx.x == 0) {
-            a.trace[4 * (int64_t)sidx + 0] = __builtin_amdgcn_s_memrealtime();
-            a.trace[4 * (int64_t)sidx + 3] = (uint64_t)blockIdx.x | ((uint64_t)__smid() << 32);
+            a.trace[8 * (int64_t)sidx + 0] = __builtin_amdgcn_s_memrealtime();
+            a.trace[8 * (int64_t)sidx + 3] = (uint64_t)blockIdx.x | ((uint64_t)__smid() << 32);
         }
 
-        const int g = sidx * W + w;                // wave stripe (compute waves)
-        const bool real = !loader && g < a.NG;
-        const bool next_real = !loader && w + 1 < W && g + 1 < a.NG;
+        const int g0 = sidx * a.SQ + min(sidx, a.SR);                 // first stripe of the WG-stripe
+        const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - g0);  // its stripes (<= W)
+        const int g = g0 + w;                      // wave stripe (compute waves)
+        const bool real = !loader && w < nw;
+        const bool next_real = !loader && w + 1 < nw;
         const int j0 = 1 + 64 * g;                 // first row of the wave stripe
         const int jrow = j0 + lane;
         int gav = 0;
@@ -306,7 +313,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             // ---------------- compute wave: its 64-row stripe, chunk by chunk ----
             uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
             int32_t* tile = a.H + (int64_t)g * a.spitch;
-            const bool publish = (w == W - 1) && sidx + 1 < a.NSW;
+            const bool publish = (w == nw - 1) && sidx + 1 < a.NSW;
             // The wave holding the panel's last row (lane 63: panels above the
             // last one have a multiple of 64 rows) feeds the panel below.
             const bool xpublish = a.xout && g == a.NG - 1;
@@ -326,8 +333,8 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
                 asm volatile("" : "+v"(kc.kd[s]));     // keep the constants in VGPRs
             }
             ChunkRegs r;
-            // column 0: H[0][j] = -j*d (computation.c:112-120) -> G' = -(1 + row_base + 64*sidx*W)*d
-            r.gin = -(1 + a.row_base + 64 * sidx * W) * d;
+            // column 0: H[0][j] = -j*d (computation.c:112-120) -> G' = -(1 + row_base + 64*g0)*d
+            r.gin = -(1 + a.row_base + 64 * g0) * d;
             r.gp6 = r.gin;
             r.tm = r.gin;
             r.dgA = r.dgB = 0;
@@ -338,7 +345,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             // Ring writes: lane 63 into the slot, the other lanes into a
             // per-lane dummy, so no exec juggling per chunk.  One address per
             // ring slot (the chunk loop is unrolled by R).
-            const int ring0 = lane == 63 ? lds_addr(tout) : lds_addr(&scratch[lane * CH]);
+            const int ring0 = lane == 63 ? lds_addr(tout) : lds_addr(&scratch[lane]);
             int ra[R];
 #pragma unroll
             for (int q = 0; q < R; ++q) {
@@ -348,7 +355,10 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             const int32_t* hb = tile;                   // score tile of the current chunk
             uint32_t* dchunk = a.D + (int64_t)g * NC * 64;      // codes of the previous chunk (c - 1)
             const uint8_t* s1c = a.s1;                  // top-string bytes of chunk c
-            if (a.trace && lane == 0 && w == 0) a.trace[4 * (int64_t)sidx + 1] = __builtin_amdgcn_s_memrealtime();
+            if (a.trace && lane == 0 && w == 0) {
+                a.trace[8 * (int64_t)sidx + 1] = __builtin_amdgcn_s_memrealtime();
+                a.trace[8 * (int64_t)sidx + 4] = __builtin_amdgcn_s_memtime();
+            }
             // Chunk prologue, software-pipelined one chunk ahead: the s1 bytes
             // (s_load), our producer's progress, the ring slot and our
             // consumer's progress for chunk c+1 are all requested at the start
@@ -502,7 +512,10 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             }
             gav = r.gav;
         }
-        if (a.trace && threadIdx.x == 64 * (W - 1)) a.trace[4 * (int64_t)sidx + 2] = __builtin_amdgcn_s_memrealtime();
+        if (a.trace && !loader && w == nw - 1 && lane == 0) {
+            a.trace[8 * (int64_t)sidx + 2] = __builtin_amdgcn_s_memrealtime();
+            a.trace[8 * (int64_t)sidx + 5] = __builtin_amdgcn_s_memtime();
+        }
         if (ST && real) {
             const bool rowok = jrow <= a.L2;
             int gv = rowok ? gav : 0;
@@ -629,9 +642,13 @@ KernelFn pick_kernel(int W, bool sh, bool sd, bool stt) {
     switch (W) {
         case 1: return pick_flags<1>(sh, sd, stt);
         case 2: return pick_flags<2>(sh, sd, stt);
+        case 3: return pick_flags<3>(sh, sd, stt);
         case 4: return pick_flags<4>(sh, sd, stt);
+        case 5: return pick_flags<5>(sh, sd, stt);
         case 6: return pick_flags<6>(sh, sd, stt);
+        case 7: return pick_flags<7>(sh, sd, stt);
         case 8: return pick_flags<8>(sh, sd, stt);
+        case 10: return pick_flags<10>(sh, sd, stt);
         case 12: return pick_flags<12>(sh, sd, stt);
         case 15: return pick_flags<15>(sh, sd, stt);
         default: return nullptr;
@@ -639,18 +656,31 @@ KernelFn pick_kernel(int W, bool sh, bool sd, bool stt) {
 }
 
 // Compute waves per workgroup (+1 loader wave; 16 waves = 1024 threads max).
-const int kWaveChoices[] = {1, 2, 4, 6, 8, 12, 15};
+const int kWaveChoices[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 15};
 
-int choose_waves(int64_t NG, int ncu) {
+// How the NG 64-row stripes become workgroup stripes.  One WG-stripe per CU
+// when that takes at most 15 waves, the stripes dealt as evenly as possible
+// (SQ or SQ+1 each), so every CU works and each SIMD holds <= 4 stripes;
+// otherwise fixed 8-stripe WG-stripes taken in turn from the dequeue.
+struct StripePlan {
+    int W;              // kernel's compute waves per workgroup
+    int64_t NSW;        // WG-stripes
+    int SQ, SR;         // see FillArgs
+};
+
+StripePlan plan_stripes(int64_t NG, int ncu) {
+    StripePlan p{8, (NG + 7) / 8, 8, 0};
     if (const char* e = getenv("NW_WAVES")) {
         const int w = atoi(e);
         for (int c : kWaveChoices)
-            if (c == w) return w;
+            if (c == w) return StripePlan{w, (NG + w - 1) / w, w, 0};
     }
-    // One workgroup per CU when the stripes allow it, else the widest WG.
+    if (NG <= ncu) return StripePlan{1, NG, 1, 0};
+    const int SQ = (int)(NG / ncu), SR = (int)(NG % ncu);
+    const int need = SQ + (SR > 0);
     for (int c : kWaveChoices)
-        if ((NG + c - 1) / c <= ncu) return c;
-    return 8;
+        if (c >= need) return StripePlan{c, ncu, SQ, SR};
+    return p;
 }
 
 TableView view_of(const nw_table* t) {
@@ -701,7 +731,8 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
     NW_HIPCHK(hipMemsetAsync(t->ctl, 0, CTL_WORDS * 4, t->stream));
     int W = 0;
     if (L1 > 0 && L2 > 0) {
-        W = choose_waves(t->NG, t->ncu);
+        const StripePlan plan = plan_stripes(t->NG, t->ncu);
+        W = plan.W;
         KernelFn fn = pick_kernel(W, sh, sd, stt);
         if (!fn) return fail(NW_ERR_ARG, "nw_table_fill: unsupported wave count");
         FillArgs a{};
@@ -714,7 +745,9 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         a.d = d;
         a.NC = (int32_t)t->NC;
         a.NG = (int32_t)t->NG;
-        a.NSW = (int32_t)((t->NG + W - 1) / W);
+        a.NSW = (int32_t)plan.NSW;
+        a.SQ = plan.SQ;
+        a.SR = plan.SR;
         a.H = t->H;
         a.spitch = t->spitch;
         a.D = t->D;
@@ -733,7 +766,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         a.xblk = (int32_t)std::max<int64_t>(t->xblk, 1);
         if (t->xout && (L2 % 64) != 0) return fail(NW_ERR_ARG, "nw_table_fill: a feeding panel needs 64*k rows");
         if (getenv("NW_TRACE")) {
-            const int64_t need = 4 * (int64_t)a.NSW;
+            const int64_t need = 8 * (int64_t)a.NSW;
             if (t->trace_n < need) {
                 (void)hipFree(t->trace);
                 t->trace = nullptr;

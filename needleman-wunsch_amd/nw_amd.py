@@ -26,7 +26,7 @@ from dataclasses import dataclass
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libnwfill.so")
+LIB_PATH = os.environ.get("NW_LIB") or os.path.join(HERE, "lib", "libnwfill.so")
 
 NW_OUT_SCORES = 1
 NW_OUT_DIRS = 2
@@ -279,12 +279,13 @@ class Table:
         return out
 
     def trace(self) -> np.ndarray:
-        """In-kernel timeline (needs $NW_TRACE): rows (dequeue, start, end, block|cu<<32)."""
+        """In-kernel timeline (needs $NW_TRACE): rows (dequeue, start, end, block|cu<<32,
+        clk_start, clk_end, 0, 0) -- realtime at 100 MHz, clk = shader clock."""
         n = self._lib.nw_table_trace(self._h, None, 0)
         out = np.zeros(max(n, 0), dtype=np.uint64)
         if n > 0:
             self._lib.nw_table_trace(self._h, out.ctypes.data, n)
-        return out.reshape(-1, 4)
+        return out.reshape(-1, 8)
 
     @property
     def waves(self) -> int:

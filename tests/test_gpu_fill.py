@@ -68,11 +68,17 @@ def test_params_vs_oracle(m, k, d):
     _check_against_oracle(O.gen_dna(3, 700), O.gen_dna(4, 900), m, k, d)
 
 
-@pytest.mark.parametrize("w", [1, 2, 4, 6, 8, 12, 15])
+@pytest.mark.parametrize("w", [1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 15])
 def test_every_workgroup_height(waves, w):
     """Each WG height; L2 spans many WG-stripes so the granule hand-off runs."""
     waves(w)
     _check_against_oracle(O.gen_dna(5, 1234), O.gen_dna(6, 64 * w * 5 + 17), 2, 3, 5)
+
+
+@pytest.mark.parametrize("L1,L2", [(300, 64 * 300 + 5), (200, 64 * 1000 + 3), (130, 100_000), (61, 64 * 256 * 3)])
+def test_balanced_stripe_plan(L1, L2):
+    """More stripes than CUs: one WG-stripe per CU holding SQ or SQ+1 stripes."""
+    _check_against_oracle(O.gen_dna(15, L1), O.gen_dna(16, L2), 2, 3, 5)
 
 
 def test_many_workgroup_stripes_handoff(waves):

@@ -17,7 +17,8 @@ Every DPP that reads a VGPR the previous VALU wrote needs two wait states
 the direction code, score and |H| of step s-1 (the up flag needs sh_s, so
 that work trails by one step) and the substitution score of step s+1.  The
 3-bit code of a cell is shifted into a per-lane word with v_addc
-(acc = 2*acc + flag: left, up, diag), so 8 codes fill bits 0..23.
+(acc = 2*acc + flag: left, up, diag; see code_items), so 8 codes fill
+bits 0..23.
 
 Register roles are fixed so that nothing is copied between chunks: G'_6 and
 G'_7 are written into the carried operands gp6 / gin, the code word of the
@@ -64,19 +65,45 @@ def byte_src(s):
     return ("chlo", 8 * s) if s < 4 else ("chhi", 8 * (s - 4))
 
 
-def code_items(s, sh):
-    """Flags of column s-1 (sh = register holding wave_shr1 of G'_{s-1}) into its word."""
+CODES = "align"    # or "cmp" (v_cmp + v_addc, the previous scheme; A/B runs)
+
+
+def code_items_cmp(s, sh):
+    """Flags of column s-1 via v_cmp -> SGPR mask -> v_addc shift-in (A/B reference)."""
     Gp, Gpp, DGp = gname(s - 1), gname(s - 2), dg_reg(s - 1)
-    fresh = s == 1            # first code of this chunk's word
+    fresh = "0, 0" if s == 1 else "%[accp], %[accp]"
     items = [("L", f"v_cmp_eq_i32_e64 %[sL], %[{Gp}], %[{Gpp}]", [], False),
              ("D", f"v_cmp_eq_i32_e64 %[sD], %[{Gp}], %[{DGp}]", [], False),
-             ("U", f"v_cmp_eq_i32_e64 %[sU], %[{Gp}], %[{sh}]", [], True)]
-    if fresh:
-        items.append(("b1", "v_addc_co_u32_e64 %[accp], vcc, 0, 0, %[sL]", ["L"], False))
-    else:
-        items.append(("b1", "v_addc_co_u32_e64 %[accp], vcc, %[accp], %[accp], %[sL]", ["L"], False))
-    items.append(("b2", "v_addc_co_u32_e64 %[accp], vcc, %[accp], %[accp], %[sU]", ["U", "b1"], True))
-    items.append(("b3", "v_addc_co_u32_e64 %[accp], vcc, %[accp], %[accp], %[sD]", ["D", "b2"], True))
+             ("U", f"v_cmp_eq_i32_e64 %[sU], %[{Gp}], %[{sh}]", [], True),
+             ("b1", f"v_addc_co_u32_e64 %[accp], vcc, {fresh}, %[sL]", ["L"], False),
+             ("b2", "v_addc_co_u32_e64 %[accp], vcc, %[accp], %[accp], %[sU]", ["U", "b1"], True),
+             ("b3", "v_addc_co_u32_e64 %[accp], vcc, %[accp], %[accp], %[sD]", ["D", "b2"], True),
+             ("G1", "s_nop 0", [], False)]
+    if s == 0:
+        items.append(("MV", "v_mov_b32_e32 %[acc], %[accp]", ["b3"], True))
+    return items
+
+
+def code_items(s, sh):
+    """Flags of column s-1 (sh = register holding wave_shr1 of G'_{s-1}) into its word.
+
+    Every candidate X is <= G'_{s-1} (it is a max over them), so X == G' exactly
+    when (G' - 1) - X < 0: the flag is the sign bit of one cheap VOP2
+    subtraction, shifted into the word by v_alignbit_b32 (acc << 1 | d >> 31).
+    Neighbouring scores differ by a few |m|+|k|+|d|, so the subtraction cannot
+    wrap.  No compares, no SGPR masks.
+    """
+    if CODES == "cmp":
+        return code_items_cmp(s, sh)
+    Gp, Gpp, DGp = gname(s - 1), gname(s - 2), dg_reg(s - 1)
+    hi = "0" if s == 1 else "%[accp]"      # first code of this chunk's word starts from 0
+    items = [("G1", f"v_add_u32_e32 %[gm1], -1, %[{Gp}]", [], False),
+             ("L", f"v_sub_u32_e32 %[dL], %[gm1], %[{Gpp}]", ["G1"], False),
+             ("D", f"v_sub_u32_e32 %[dD], %[gm1], %[{DGp}]", ["G1"], False),
+             ("U", f"v_sub_u32_e32 %[dU], %[gm1], %[{sh}]", ["G1"], True),
+             ("b1", f"v_alignbit_b32 %[accp], {hi}, %[dL], 31", ["L"], False),
+             ("b2", "v_alignbit_b32 %[accp], %[accp], %[dU], 31", ["U", "b1"], True),
+             ("b3", "v_alignbit_b32 %[accp], %[accp], %[dD], 31", ["D", "b2"], True)]
     if s == 0:                # the previous chunk's word is complete: hand it out
         items.append(("MV", "v_mov_b32_e32 %[acc], %[accp]", ["b3"], True))
     return items
@@ -181,10 +208,10 @@ def flush(N, F, H, A, S):
     s = N
     out = [ring_item(s)[1]]
     if F:
-        items = code_items(s, f"t{s - 1}")
-        L, D, U, b1, b2, b3 = [t for _, t, _, _ in items[:6]]
-        out += [L, D, f"v_mov_b32_dpp %[t{s - 1}], %[{gname(s - 1)}] wave_shr:1 row_mask:0xf bank_mask:0xf",
-                U, b1, b2, b3]
+        items = {n: t for n, t, _, _ in code_items(s, f"t{s - 1}")}
+        out += [items["G1"], items["L"], items["D"],
+                f"v_mov_b32_dpp %[t{s - 1}], %[{gname(s - 1)}] wave_shr:1 row_mask:0xf bank_mask:0xf",
+                items["U"], items["b1"], items["b2"], items["b3"]]
     if H:
         out += [t for _, t, _, _ in score_items(s, A, S)]
     return out
@@ -200,7 +227,8 @@ OPERANDS = r'''
       [h0] "=&v"(r.h[0]), [h1] "=&v"(r.h[1]), [h2] "=&v"(r.h[2]), [h3] "=&v"(r.h[3]),                      \
       [h4] "=&v"(r.h[4]), [h5] "=&v"(r.h[5]), [h6] "=&v"(r.h[6]), [h7] "=&v"(r.h[7]),                      \
       [accp] "+v"(r.accp), [acc] "=&v"(r.acc), [gav] "+v"(r.gav), [tmp] "=&v"(tmp_),                      \
-      [sL] "=&s"(sL_), [sU] "=&s"(sU_), [sD] "=&s"(sD_), [sM] "=&s"(sM_), [sC] "=&s"(sC_)                  \
+      [gm1] "=&v"(gm1_), [dL] "=&v"(dL_), [dU] "=&v"(dU_), [dD] "=&v"(dD_), [sM] "=&s"(sM_), [sC] "=&s"(sC_), \
+      [sL] "=&s"(sL_), [sU] "=&s"(sU_), [sD] "=&s"(sD_)                                                  \
     : [c2] "v"(k.c2), [vcm] "v"(k.vcm), [vck] "v"(k.vck), [nlo] "v"(k.nlo),                               \
       [chlo] "s"(ch.lo), [chhi] "s"(ch.hi), [chn] "s"(ch.nlo),                                            \
       [k0] "v"(k.kd[0]), [k1] "v"(k.kd[1]), [k2] "v"(k.kd[2]), [k3] "v"(k.kd[3]),                          \
@@ -222,6 +250,13 @@ def tf(b):
 
 
 def main():
+    global OUT, CODES
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--codes", choices=("align", "cmp"), default="align")
+    ap.add_argument("--out", default=OUT)
+    args = ap.parse_args()
+    OUT, CODES = args.out, args.codes
     parts = ["// GENERATED by tools/gen_chunk_asm.py -- do not edit; see the generator for the schedule.\n",
              OPERANDS, FLUSH_OPERANDS,
              "template <bool SH, bool SD, bool ST, int N, bool NEXT>\n"
@@ -229,7 +264,7 @@ def main():
              "                                          int ra, const int32_t* hb);\n"
              "template <bool SH, bool SD, bool ST, int N>\n"
              "__device__ __forceinline__ void flush_asm(ChunkRegs& r, const ChunkConst& k, int ra, const int32_t* hb);\n"]
-    decl = "    int tmp_; uint64_t sL_, sU_, sD_, sM_; uint32_t sC_;\n"
+    decl = "    int tmp_, gm1_, dL_, dU_, dD_; uint64_t sM_, sL_, sU_, sD_; uint32_t sC_;\n"
     for SH in (0, 1):
         for SD in (0, 1):
             for ST in (0, 1):

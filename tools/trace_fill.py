@@ -16,9 +16,13 @@ deq, st, en = (tr[:, 0] - t0) / 100.0, (tr[:, 1] - t0) / 100.0, (tr[:, 2] - t0) 
 dur = en - st
 n = len(tr)
 print(f"L1={L1} L2={L2} mask={mask} waves={t.waves} stripes={n} kernel_ms={k:.3f}")
-print(f"start of stripe i (us): " + " ".join(f"{st[i]:.1f}" for i in [0, 1, 2, n // 4, n // 2, 3 * n // 4, n - 1]))
-print(f"end   of stripe i (us): " + " ".join(f"{en[i]:.1f}" for i in [0, 1, 2, n // 4, n // 2, 3 * n // 4, n - 1]))
-lag = np.diff(st)
+idx = sorted(set(min(n - 1, i) for i in [0, 1, 2, n // 4, n // 2, 3 * n // 4, n - 1]))
+print(f"start of stripe i (us): " + " ".join(f"{st[i]:.1f}" for i in idx))
+print(f"end   of stripe i (us): " + " ".join(f"{en[i]:.1f}" for i in idx))
+clk = (tr[:, 5] - tr[:, 4]).astype(np.float64)
+mhz = clk / np.maximum(dur, 1e-9)
+print(f"shader clock over stripe i (MHz): " + " ".join(f"{mhz[i]:.0f}" for i in idx))
+lag = np.diff(st) if n > 1 else np.zeros(1)
 print(f"start lag per stripe: mean {lag.mean():.2f} us  median {np.median(lag):.2f}  p90 {np.percentile(lag, 90):.2f}  max {lag.max():.2f}")
 print(f"stripe duration: first {dur[0]:.1f} us  median {np.median(dur):.1f}  last {dur[-1]:.1f}  max {dur.max():.1f}")
 cu = (tr[:, 3] >> 32) & 0xffffffff
