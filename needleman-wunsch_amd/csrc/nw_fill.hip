@@ -106,28 +106,40 @@ constexpr int SUPER_CHUNKS = 512;     // chunks per super-chunk (4096 columns)
 
 __device__ __forceinline__ int chunk_base(int c) { return (c / SUPER_CHUNKS) * (SUPER_CHUNKS * CH); }
 
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v2i __attribute__((ext_vector_type(2)));
+
+// Ring slot: 8 T' of a chunk + its 8 top-string bytes (2 words), 16-int stride.
+// In registers as the three vectors the block's wide LDS reads fill.
+constexpr int SLOT = 16;
+struct RingSlot {
+    v4i a, b;           // T' of steps 0..3, 4..7
+    v2i c;              // top-string bytes of columns 1..4, 5..8 of the chunk
+};
+
 struct ChunkRegs {
     int g[6];           // out: G' after steps 0..5 (lane 63 -> the wave below)
     int gp6, gin;       // in: G' of the previous chunk's columns 7, 8; out: this chunk's
-    int t[8];           // in: T' of each step (t[s-1] is reused for wave_shr1 of step s)
     int tm;             // in: T' of the previous column; out: T' of this chunk's last
     int dgA, dgB;       // diagonal candidates of even / odd steps (dgB: last step of a full chunk)
-    int subA, subB;     // sub' of even / odd steps (subA: step 0 of the next chunk)
+    int subA, subB;     // sub' of even / odd steps
     int h[8];           // out: H of steps 0..7 (partial chunks: the flush block adds the last)
     uint32_t accp;      // in: previous chunk's codes (missing the last); out: this chunk's so far
     uint32_t acc;       // out: previous chunk's complete codes word
     int gav;            // in/out: running max |H| (stats)
+    uint64_t pq;        // out: {prog[w], cons[w+1]} read mid-chunk (NEXT blocks)
+    int cv;             // in/out: chunk index + 1 (ring counter value of this chunk)
+    int hv, dv;         // in/out: byte offsets of this lane in the score / code tiles
+    int nlo;            // in/out: -(r*d) - (8c - base)*d: H = G' + nlo - (s+1)*d
 };
 struct ChunkConst {
     uint32_t c2;        // this lane's side-string byte
     int vcm, vck;       // sub' for match / mismatch
-    int nlo;            // -(r*d) - (8c - base)*d: H = G' + nlo - (s+1)*d
+    int d8;             // 8*d (nlo step per chunk)
     int kd[8];          // -(s+1)*d
-    int hv;             // lane*4: byte offset of this lane in a score-tile column
-};
-struct ChunkChars {
-    uint32_t lo, hi;    // this chunk's 8 top-string bytes
-    uint32_t nlo;       // next chunk's first 4 bytes
+    int cb;             // LDS address of ctr[2w] (ring counters, see the kernel)
+    int32_t* hb;        // score tile base (moves every super-chunk, with hv)
+    uint32_t* db;       // code tile base (moves every super-chunk, with dv)
 };
 
 #include "nw_chunk.inc"
@@ -138,7 +150,6 @@ __device__ __forceinline__ uint32_t branch_codes(uint32_t x) {
     return __builtin_popcount(y & 0x249249u);
 }
 
-// The last chunk of a stripe (n = 1..8 columns): block + flush.
 // G' of step s of the current chunk (steps 6, 7 live in the carried registers).
 __device__ __forceinline__ int g_of(const ChunkRegs& r, int s) {
     switch (s) {
@@ -153,28 +164,46 @@ __device__ __forceinline__ int g_of(const ChunkRegs& r, int s) {
     }
 }
 
-// Returns H of the stripe's last column (for the score-only last column).
+// The last chunk of a stripe (n = 1..8 columns): block + flush.  Returns H
+// of the stripe's last column (for the score-only last column).
 template <bool SH, bool SD, bool ST, int N>
-__device__ __forceinline__ int run_last(ChunkRegs& r, const ChunkConst& k, const ChunkChars& ch, int ra,
-                                        const int32_t* hb) {
-    chunk_asm<SH, SD, ST, N, false>(r, k, ch, ra, hb);
-    flush_asm<SH, SD, ST, N>(r, k, ra, hb);
+__device__ __forceinline__ int run_last(ChunkRegs& r, const ChunkConst& k, const RingSlot& t, int ra) {
+    RingSlot n;
+    chunk_asm<SH, SD, ST, N, false>(r, k, t, n, ra, 0);
+    flush_asm<SH, SD, ST, N>(r, k, t, ra);
     if constexpr (SH || ST) return r.h[N - 1];
-    else return g_of(r, N - 1) + k.nlo + k.kd[N - 1];
+    else return g_of(r, N - 1) + r.nlo + k.kd[N - 1];
 }
 template <bool SH, bool SD, bool ST>
-__device__ __forceinline__ int run_last_n(int n, ChunkRegs& r, const ChunkConst& k, const ChunkChars& ch, int ra,
-                                          const int32_t* hb) {
+__device__ __forceinline__ int run_last_n(int n, ChunkRegs& r, const ChunkConst& k, const RingSlot& t, int ra) {
     switch (n) {
-        case 1: return run_last<SH, SD, ST, 1>(r, k, ch, ra, hb);
-        case 2: return run_last<SH, SD, ST, 2>(r, k, ch, ra, hb);
-        case 3: return run_last<SH, SD, ST, 3>(r, k, ch, ra, hb);
-        case 4: return run_last<SH, SD, ST, 4>(r, k, ch, ra, hb);
-        case 5: return run_last<SH, SD, ST, 5>(r, k, ch, ra, hb);
-        case 6: return run_last<SH, SD, ST, 6>(r, k, ch, ra, hb);
-        case 7: return run_last<SH, SD, ST, 7>(r, k, ch, ra, hb);
-        default: return run_last<SH, SD, ST, 8>(r, k, ch, ra, hb);
+        case 1: return run_last<SH, SD, ST, 1>(r, k, t, ra);
+        case 2: return run_last<SH, SD, ST, 2>(r, k, t, ra);
+        case 3: return run_last<SH, SD, ST, 3>(r, k, t, ra);
+        case 4: return run_last<SH, SD, ST, 4>(r, k, t, ra);
+        case 5: return run_last<SH, SD, ST, 5>(r, k, t, ra);
+        case 6: return run_last<SH, SD, ST, 6>(r, k, t, ra);
+        case 7: return run_last<SH, SD, ST, 7>(r, k, t, ra);
+        default: return run_last<SH, SD, ST, 8>(r, k, t, ra);
     }
+}
+
+// Slow path of the ring: this wave's {prog, cons} counter pair, then the
+// ring slot at LDS address rd (LDS is in order per wave: slot data read after
+// a progress value that covers it is valid).  Same registers as the block's
+// own reads of the next slot, and waited for here.
+__device__ __forceinline__ uint64_t read_slot(int cb, int rd, RingSlot& s) {
+    uint64_t pq;
+    asm volatile(
+        "ds_read_b64 %[pq], %[cb] offset:8\n\t"
+        "ds_read_b128 %[a], %[rd]\n\t"
+        "ds_read_b128 %[b], %[rd] offset:16\n\t"
+        "ds_read_b64 %[c], %[rd] offset:32\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : [pq] "=&v"(pq), [a] "=&v"(s.a), [b] "=&v"(s.b), [c] "=&v"(s.c)
+        : [cb] "v"(cb), [rd] "v"(rd)
+        : "memory");
+    return pq;
 }
 
 // Hand-off granule load: agent scope between workgroups of one fill, system
@@ -197,25 +226,31 @@ __device__ __forceinline__ void lds_publish(int* p, int v) {
 
 // Workgroup = W compute waves (64-row stripes, stacked) + 1 loader wave, no
 // barriers inside a stripe.  Wave w takes the top row of each 8-column chunk
-// from an LDS ring tring[w] (R chunk slots) filled by its producer (the
-// loader for w = 0, wave w-1 otherwise) and puts its own bottom row into
-// tring[w+1].  prog[w] = chunks available in tring[w], cons[w] = chunks wave w
-// has taken out of it; a producer only waits when it is R chunks ahead.
-// The loader feeds tring[0] from the previous WG-stripe's granules; it issues
-// no stores, so its waits on the hand-off loads are exact, and the compute
-// waves never wait on vmcnt.  Granules (between workgroups and panels) carry
-// H - d of the row above in the plain domain; ring slots carry G'.
+// (and the chunk's top-string bytes) from an LDS ring tring[w] (R chunk
+// slots) filled by its producer (the loader for w = 0, wave w-1 otherwise)
+// and puts its own bottom row into tring[w+1].  Ring counters, interleaved so
+// that a wave reads both of its own in one 8-byte LDS read:
+//     ctr[2v+2] = prog[v]: chunks available in tring[v],
+//     ctr[2v+1] = cons[v]: chunks wave v has taken out of tring[v]
+// (cons of a wave that does not exist = "infinite").  A producer only waits
+// when it is R chunks ahead.  The chunk block (nw_chunk.inc) issues all of a
+// chunk's LDS traffic itself, including the next slot's reads; the C++ below
+// only checks the progress values it read.  The loader feeds tring[0] from
+// the previous WG-stripe's granules; it issues no stores, so its waits on the
+// hand-off loads are exact, and the compute waves never wait on vmcnt.
+// Granules (between workgroups and panels) carry H - d of the row above in
+// the plain domain; ring slots carry G'.
 template <int W, bool SH, bool SD, bool ST>
 __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
     constexpr int R = 4;
     constexpr bool F = SD || ST;     // direction codes
-    __shared__ __attribute__((aligned(16))) int tring[(W + 1) * R * CH];
+    constexpr int NOCONS = 1 << 30;
+    __shared__ __attribute__((aligned(16))) int tring[(W + 1) * R * SLOT];
     // Dummy target of the ring writes of lanes 0..62: lane-contiguous, so a
     // ds_write_b32 of the whole wave is bank-conflict free (an 8-dword lane
     // stride made every ring write a 16-way conflict).
-    __shared__ int scratch[64 + R * CH + CH];
-    __shared__ int prog[W + 1];
-    __shared__ int cons[W + 1];
+    __shared__ int scratch[64 + R * SLOT];
+    __shared__ __attribute__((aligned(8))) int ctr[2 * W + 4];
     __shared__ int sh_sidx;
     __shared__ int sh_abort;
 
@@ -230,12 +265,14 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
 
     for (;;) {
         if (threadIdx.x == 0) {
-            sh_sidx = (int)atomicAdd(&a.ctl[CTL_NEXT], 1u);
+            const int sidx = (int)atomicAdd(&a.ctl[CTL_NEXT], 1u);
+            sh_sidx = sidx;
             sh_abort = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-        }
-        if (threadIdx.x <= W) {
-            prog[threadIdx.x] = 0;
-            cons[threadIdx.x] = 0;
+            const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - (sidx * a.SQ + min(sidx, a.SR)));
+            for (int v = 0; v <= W; ++v) {
+                ctr[2 * v + 2] = 0;
+                ctr[2 * v + 1] = v < nw ? 0 : NOCONS;
+            }
         }
         __syncthreads();
         const int sidx = uni(sh_sidx);
@@ -249,7 +286,6 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
         const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - g0);  // its stripes (<= W)
         const int g = g0 + w;                      // wave stripe (compute waves)
         const bool real = !loader && w < nw;
-        const bool next_real = !loader && w + 1 < nw;
         const int j0 = 1 + 64 * g;                 // first row of the wave stripe
         const int jrow = j0 + lane;
         int gav = 0;
@@ -259,17 +295,21 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             // ---------------- loader wave: no stores, exact waits ----------------
             // Source of the WG-stripe's top row: the seeded row 0, the panel
             // above (xin, written by another agent: system-scope loads), or
-            // the previous WG-stripe's granules (agent scope).
+            // the previous WG-stripe's granules (agent scope).  Lanes 8, 9
+            // carry the chunk's top-string bytes.
             const bool seeded = sidx == 0 && !a.xin;
             const bool xsrc = sidx == 0 && a.xin;
             const uint64_t* gin = xsrc ? a.xin : a.gran + (int64_t)(sidx % a.nslot) * a.gpitch;
             const uint32_t want = xsrc ? a.epoch : (uint32_t)sidx;
+            const uint32_t* s1w = reinterpret_cast<const uint32_t*>(a.s1);
+            const bool chl = lane == 8 || lane == 9;
             uint64_t pf = 0;
+            uint32_t pc = chl ? s1w[lane - 8] : 0u;
             if (!seeded && lane < CH) pf = ld_gran(gin + lane, xsrc);
             for (int c = 0; c < NC; ++c) {
                 const int n = (c == NC - 1) ? nlast : CH;
-                while (lds_ld(&cons[0]) < c - R + 1) __builtin_amdgcn_s_sleep(1);   // ring slot free?
-                int* dst = &tring[(c % R) * CH];
+                while (lds_ld(&ctr[1]) < c - R + 1) __builtin_amdgcn_s_sleep(1);   // ring slot free?
+                int* dst = &tring[(c % R) * SLOT];
                 const int base = chunk_base(c);
                 if (seeded) {
                     // row 0: H[i][0] - d = -(i+1)*d (computation.c:102-110) -> G' = -(base+1)*d
@@ -307,110 +347,113 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
                     if (c + 1 < NC && lane < CH)          // prefetch the next chunk
                         pf = ld_gran(gin + CH * (int64_t)(c + 1) + lane, xsrc);
                 }
-                if (lane == 0) lds_publish(&prog[0], c + 1);
+                if (chl) {
+                    dst[lane] = (int)pc;
+                    if (c + 1 < NC) pc = s1w[2 * (c + 1) + lane - 8];
+                }
+                if (lane == 0) lds_publish(&ctr[2], c + 1);
             }
         } else if (real) {
             // ---------------- compute wave: its 64-row stripe, chunk by chunk ----
             uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
             int32_t* tile = a.H + (int64_t)g * a.spitch;
+            // codes: row q+1 of the stripe's code tile holds chunk q (row 0 pads
+            // the block's store of the word "before" chunk 0)
+            uint32_t* dtile = a.D + (int64_t)g * (NC + 1) * 64;
             const bool publish = (w == nw - 1) && sidx + 1 < a.NSW;
             // The wave holding the panel's last row (lane 63: panels above the
             // last one have a multiple of 64 rows) feeds the panel below.
             const bool xpublish = a.xout && g == a.NG - 1;
             const bool out_lane = jrow <= a.L2;
-            const int* tin = &tring[w * R * CH];
-            int* tout = &tring[(w + 1) * R * CH];
+            const int* tin = &tring[w * R * SLOT];
+            const int* tout = &tring[(w + 1) * R * SLOT];
             ChunkConst kc;
             kc.c2 = a.s2[jrow - 1];
             asm volatile("" : "+v"(vcm), "+v"(vck));   // VGPR operands of v_cndmask
             kc.vcm = vcm;
             kc.vck = vck;
-            kc.nlo = -(64 * w + lane) * d;
-            kc.hv = lane * 4;
+            kc.d8 = CH * d;
 #pragma unroll
             for (int s = 0; s < CH; ++s) {
                 kc.kd[s] = -(s + 1) * d;
                 asm volatile("" : "+v"(kc.kd[s]));     // keep the constants in VGPRs
             }
+            kc.cb = lds_addr(&ctr[2 * w]);
+            asm volatile("" : "+v"(kc.cb));
+            kc.hb = tile;
+            kc.db = dtile;
             ChunkRegs r;
             // column 0: H[0][j] = -j*d (computation.c:112-120) -> G' = -(1 + row_base + 64*g0)*d
             r.gin = -(1 + a.row_base + 64 * g0) * d;
             r.gp6 = r.gin;
             r.tm = r.gin;
             r.dgA = r.dgB = 0;
+            r.subA = r.subB = 0;
             r.accp = 0;
             r.gav = 0;
-            r.subA = ((uint32_t)a.s1[0] == kc.c2) ? vcm : vck;
-            r.subB = 0;
+            r.pq = 0;
+            r.cv = 1;
+            r.hv = lane * 4;
+            r.dv = lane * 4;
+            r.nlo = -(64 * w + lane) * d;
             // Ring writes: lane 63 into the slot, the other lanes into a
             // per-lane dummy, so no exec juggling per chunk.  One address per
             // ring slot (the chunk loop is unrolled by R).
             const int ring0 = lane == 63 ? lds_addr(tout) : lds_addr(&scratch[lane]);
-            int ra[R];
+            int ra[R], rd[R];
 #pragma unroll
             for (int q = 0; q < R; ++q) {
-                ra[q] = ring0 + q * CH * 4;
-                asm volatile("" : "+v"(ra[q]));
+                ra[q] = ring0 + q * SLOT * 4;
+                rd[q] = lds_addr(tin) + q * SLOT * 4;
+                asm volatile("" : "+v"(ra[q]), "+v"(rd[q]));
             }
-            const int32_t* hb = tile;                   // score tile of the current chunk
-            uint32_t* dchunk = a.D + (int64_t)g * NC * 64;      // codes of the previous chunk (c - 1)
-            const uint8_t* s1c = a.s1;                  // top-string bytes of chunk c
             if (a.trace && lane == 0 && w == 0) {
                 a.trace[8 * (int64_t)sidx + 1] = __builtin_amdgcn_s_memrealtime();
                 a.trace[8 * (int64_t)sidx + 4] = __builtin_amdgcn_s_memtime();
             }
-            // Chunk prologue, software-pipelined one chunk ahead: the s1 bytes
-            // (s_load), our producer's progress, the ring slot and our
-            // consumer's progress for chunk c+1 are all requested at the start
-            // of chunk c and only checked at its end.  LDS is in order per
-            // wave, so ring data read after a progress value that covers it is
-            // valid.  (s_load shares lgkmcnt with LDS, so it is issued first.)
-            uint64_t ch8 = *(cptr64)(a.s1);
-            int pin = lds_ld(&prog[w]);
-            int tA[CH], tB[CH];
-#pragma unroll
-            for (int s = 0; s < CH; ++s) tA[s] = tin[s];
-            int pout = next_real ? lds_ld(&cons[w + 1]) : (1 << 30);
-            bool aborted = false;
-            // Wait until chunk c's ring slot is filled (and our consumer has
-            // room), re-reading the slot if the prefetch was too early.
-            auto wait_slot = [&](int c, int slot, int (&tt)[CH]) -> bool {
-                if (pin > c && pout >= c - R + 1) return true;
-                for (;;) {
-                    pin = lds_ld(&prog[w]);
-                    pout = next_real ? lds_ld(&cons[w + 1]) : (1 << 30);
-                    if ((pin > c && pout >= c - R + 1) || lds_ld(&sh_abort)) break;
-                    __builtin_amdgcn_s_sleep(1);
+            RingSlot tA, tB;
+            // Slow path: wait until chunk c's ring slot is filled and our
+            // consumer has room, re-reading the slot with every progress read.
+            auto wait_slot = [&](int c, int rdq, RingSlot& tt) -> bool {
+                for (int spins = 0;; ++spins) {
+                    const uint64_t pq = read_slot(kc.cb, rdq, tt);
+                    const int pin = uni((int)(uint32_t)pq), pout = uni((int)(pq >> 32));
+                    if (pin > c && pout >= c - R + 1) return true;
+                    if (uni(lds_ld(&sh_abort))) return false;
+                    if (spins > 64) __builtin_amdgcn_s_sleep(1);
                 }
-                if (lds_ld(&sh_abort)) return false;
-#pragma unroll
-                for (int s = 0; s < CH; ++s) tt[s] = tin[slot + s];
-                return true;
             };
-            // After chunk c's block: hand the ring slot to the wave below,
-            // store the previous chunk's codes, publish the WG-stripe's bottom
-            // row (last wave) and advance the per-chunk pointers.
+            auto rebase = [&](int c) {
+                if (c > 0 && c % SUPER_CHUNKS == 0) {
+                    // new super-chunk: rebase the carried G' values (and nlo) and
+                    // move the tile bases so the lane offsets stay small
+                    const int sh = SUPER_CHUNKS * CH * d;
+                    r.gin -= sh;
+                    r.gp6 -= sh;
+                    r.dgB -= sh;
+                    r.tm -= sh;
+                    r.nlo += sh;
+                    kc.hb += SUPER_CHUNKS * CH * 64;
+                    r.hv -= SUPER_CHUNKS * CH * 64 * 4;
+                    kc.db += SUPER_CHUNKS * 64;
+                    r.dv -= SUPER_CHUNKS * 64 * 4;
+                }
+            };
+            // After chunk c's block: stats of the previous chunk's codes,
+            // the last chunk's code word, and the WG-stripe's bottom row
+            // (last wave) out to the next WG-stripe / panel.
             auto after_chunk = [&](int c, int slot, int n, bool last) {
-                if (next_real) lds_publish(&prog[w + 1], c + 1);
-                if (F) {
-                    // codes trail by one column: the previous chunk's word completes now
-                    if (c > 0) {
-                        const uint32_t dw = out_lane ? r.acc : 0u;
-                        if (SD) dchunk[lane] = dw;
-                        if (ST) bc += branch_codes(dw);
-                        dchunk += 64;
-                    }
-                    if (last) {
-                        const uint32_t dw = out_lane ? (r.accp << (3 * (CH - n))) : 0u;
-                        if (SD) dchunk[lane] = dw;
-                        if (ST) bc += branch_codes(dw);
-                    }
+                if (ST && c > 0) bc += branch_codes(out_lane ? r.acc : 0u);
+                if (F && last) {
+                    const uint32_t dw = r.accp << (3 * (CH - n));
+                    if (SD) dtile[(int64_t)(c + 1) * 64 + lane] = dw;
+                    if (ST) bc += branch_codes(out_lane ? dw : 0u);
                 }
                 // (plain domain: H - d = G' - 64(w+1)d - (i - base)d)
                 if (publish || xpublish) {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     if (lane < n) {
-                        const int v = tout[slot + lane] - 64 * (w + 1) * d - (CH * c + lane + 1 - chunk_base(c)) * d;
+                        const int v = tout[slot * SLOT + lane] - 64 * (w + 1) * d -
+                                      (CH * c + lane + 1 - chunk_base(c)) * d;
                         const uint64_t tag = publish ? (uint32_t)(sidx + 1) : a.epoch;
                         const uint64_t gr = (tag << 32) | (uint32_t)v;
                         if (publish)
@@ -428,29 +471,18 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
                                                __HIP_MEMORY_SCOPE_SYSTEM);
                     }
                 }
-                kc.nlo -= CH * d;
-                hb += CH * 64;
-                s1c += CH;
             };
-            // One full (non-final) chunk; SLOT = c % R is a compile-time ring slot.
-            auto full_chunk = [&](int c, auto slotc, int (&cur)[CH], int (&nxt)[CH]) -> bool {
-                constexpr int SLOT = decltype(slotc)::value;
-                constexpr int NSLOT = ((SLOT + 1) % R) * CH;
-                if (!wait_slot(c, SLOT * CH, cur)) return false;
-#pragma unroll
-                for (int s = 0; s < CH; ++s) r.t[s] = cur[s];
-                const uint64_t ch8c = ch8;
-                // ring slot consumed (every lane stores the same word: no exec mask)
-                __hip_atomic_store(&cons[w], c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                ch8 = *(cptr64)(s1c + CH);
-                pin = lds_ld(&prog[w]);
-#pragma unroll
-                for (int s = 0; s < CH; ++s) nxt[s] = tin[NSLOT + s];
-                if (next_real) pout = lds_ld(&cons[w + 1]);
-                const ChunkChars chs{(uint32_t)ch8c, (uint32_t)(ch8c >> 32), (uint32_t)ch8};
-                chunk_asm<SH, SD, ST, 8, true>(r, kc, chs, ra[SLOT], hb);
-                after_chunk(c, SLOT * CH, CH, false);
-                return true;
+            // One full (non-final) chunk; SLOTC = c % R is a compile-time ring
+            // slot.  The block reads the next slot into nxt; the slow path
+            // re-reads it when the progress values it saw were too early.
+            auto full_chunk = [&](int c, auto slotc, const RingSlot& cur, RingSlot& nxt) -> bool {
+                constexpr int Q = decltype(slotc)::value;
+                constexpr int NQ = (Q + 1) % R;
+                chunk_asm<SH, SD, ST, 8, true>(r, kc, cur, nxt, ra[Q], rd[NQ]);
+                after_chunk(c, Q, CH, false);
+                // (wave-uniform: every lane read the same counters)
+                if (uni((int)(uint32_t)r.pq) > c + 1 && uni((int)(r.pq >> 32)) >= c + 2 - R) return true;
+                return wait_slot(c + 1, rd[NQ], nxt);
             };
             using S0 = std::integral_constant<int, 0>;
             using S1 = std::integral_constant<int, 1>;
@@ -458,57 +490,28 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             using S3 = std::integral_constant<int, 3>;
             int c = 0;
             const int nfull = NC - 1;              // chunks before the last one
+            bool aborted = !wait_slot(0, rd[0], tA);
             while (c + R <= nfull && !aborted) {
-                if (c > 0 && c % SUPER_CHUNKS == 0) {
-                    // new super-chunk: rebase the carried G' values (and nlo)
-                    const int sh = SUPER_CHUNKS * CH * d;
-                    r.gin -= sh;
-                    r.gp6 -= sh;
-                    r.dgB -= sh;
-                    r.tm -= sh;
-                    kc.nlo += sh;
-                }
+                rebase(c);
                 aborted = !full_chunk(c, S0{}, tA, tB) || !full_chunk(c + 1, S1{}, tB, tA) ||
                           !full_chunk(c + 2, S2{}, tA, tB) || !full_chunk(c + 3, S3{}, tB, tA);
                 c += R;
             }
             if (!aborted && c < nfull) {
-                if (c > 0 && c % SUPER_CHUNKS == 0) {
-                    const int sh = SUPER_CHUNKS * CH * d;
-                    r.gin -= sh;
-                    r.gp6 -= sh;
-                    r.dgB -= sh;
-                    r.tm -= sh;
-                    kc.nlo += sh;
-                }
+                rebase(c);
                 aborted = !full_chunk(c, S0{}, tA, tB);
                 if (!aborted && c + 1 < nfull) aborted = !full_chunk(c + 1, S1{}, tB, tA);
                 if (!aborted && c + 2 < nfull) aborted = !full_chunk(c + 2, S2{}, tA, tB);
                 c = nfull;
             }
-            if (!aborted) {
-                // the last chunk (n = 1..8 columns), ring slot known only at run time
-                const int slot = (c % R) * CH;
-                pin = -1;                                   // force a (re-)read of the slot
-                if (wait_slot(c, slot, tA)) {
-                    if (c > 0 && c % SUPER_CHUNKS == 0) {
-                        const int sh = SUPER_CHUNKS * CH * d;
-                        r.gin -= sh;
-                        r.gp6 -= sh;
-                        r.dgB -= sh;
-                        r.tm -= sh;
-                        kc.nlo += sh;
-                    }
-#pragma unroll
-                    for (int s = 0; s < CH; ++s) r.t[s] = tA[s];
-                    __hip_atomic_store(&cons[w], c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    const ChunkChars chs{(uint32_t)ch8, (uint32_t)(ch8 >> 32), 0u};
-                    const int n = nlast;
-                    const int rs = ring0 + slot * 4;
-                    const int hl = run_last_n<SH, SD, ST>(n, r, kc, chs, rs, hb);
-                    if (!SH) a.lastcol[j0 + lane] = hl;   // score-only: H[L1][*]
-                    after_chunk(c, slot, n, true);
-                }
+            // the last chunk (n = 1..8 columns), ring slot known only at run
+            // time: re-read into tA (whichever array the loop left it in)
+            if (!aborted && wait_slot(c, lds_addr(tin) + (c % R) * SLOT * 4, tA)) {
+                rebase(c);
+                const int slot = c % R;
+                const int hl = run_last_n<SH, SD, ST>(nlast, r, kc, tA, ring0 + slot * SLOT * 4);
+                if (!SH) a.lastcol[j0 + lane] = hl;   // score-only: H[L1][*]
+                after_chunk(c, slot, nlast, true);
             }
             gav = r.gav;
         }
@@ -583,7 +586,7 @@ __device__ __forceinline__ uint32_t code_at(const TableView& v, int64_t i, int64
     if (i == 0) return j == 0 ? 0u : 2u;          // (0,0): none; (0,j): up
     if (j == 0) return 4u;                         // (i,0): left
     const int64_t g = (j - 1) >> 6, l = (j - 1) & 63, q = (i - 1) >> 3, s = (i - 1) & 7;
-    return (v.D[(g * v.NC + q) * 64 + l] >> (21 - 3 * s)) & 7u;
+    return (v.D[(g * (v.NC + 1) + q + 1) * 64 + l] >> (21 - 3 * s)) & 7u;
 }
 
 // Dense nibble packing for nw_fill(): byte b = code(2b) | code(2b+1) << 4.
@@ -936,7 +939,7 @@ int nw_table_create(int device, int64_t max_L1, int64_t max_L2, uint32_t out_mas
             return bail(rc);
     }
     if (out_mask & NW_OUT_DIRS) {
-        if ((rc = alloc((void**)&t->D, (size_t)std::max<int64_t>(NG, 1) * std::max<int64_t>(NC, 1) * 256))) return bail(rc);
+        if ((rc = alloc((void**)&t->D, (size_t)std::max<int64_t>(NG, 1) * (NC + 1) * 256))) return bail(rc);
     }
     if ((rc = alloc((void**)&t->lastcol, (size_t)(64 * NG + 128) * 4))) return bail(rc);
     // Granule slots: one per concurrently running WG-stripe + 1.

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Generate needleman-wunsch_amd/csrc/nw_chunk.inc: the hand-scheduled
-column steps of the fill kernel, one inline-asm block per chunk.
+column steps of the fill kernel, one inline-asm block per 8-column chunk.
 
-    python tools/gen_chunk_asm.py            (rewrites the .inc)
+    python tools/gen_chunk_asm.py [--out PATH] [--read-step S]
 
 Per column step s (G' = H + r*d + (i - base)*d, r = row in the workgroup,
 i = column; see nw_fill.hip) the loop-carried chain is
@@ -13,41 +13,64 @@ i = column; see nw_fill.hip) the loop-carried chain is
     G'_s = prefix max of X_s over the 64 lanes               6 x v_max_i32_dpp
 
 Every DPP that reads a VGPR the previous VALU wrote needs two wait states
-(7 gaps per step).  The gaps hold the step's other work instead of s_nop:
-the direction code, score and |H| of step s-1 (the up flag needs sh_s, so
-that work trails by one step) and the substitution score of step s+1.  The
-3-bit code of a cell is shifted into a per-lane word with v_addc
-(acc = 2*acc + flag: left, up, diag; see code_items), so 8 codes fill
-bits 0..23.
+(7 gaps per step).  The gaps hold everything else the chunk does:
+  * the direction code, score and |H| of column s-1 (the up flag needs sh_s,
+    so that work trails by one step).  A code bit is the sign of
+    (G' - 1) - candidate (every candidate is <= G'), shifted into the word by
+    v_alignbit_b32 -- no compares, no SGPR masks;
+  * sub' of column s+1 (of column 0 in the first gap): one SDWA byte compare
+    of the chunk's top-string bytes against this lane's side-string byte and
+    a v_cndmask;
+  * all of the chunk's memory traffic.  G'_s of every lane goes to the LDS
+    ring (only lane 63's address is the real slot; the other lanes write a
+    dummy), H_s to the score tile (one coalesced 256-byte global_store_dword
+    per column), the previous chunk's code word to the code tile; the ring
+    counters (cons = this chunk taken, at the start; prog = the wave below
+    may take it, after the last ring write) and the chunk's top-string bytes
+    (which travel down the ring with T').  A chunk followed by another one
+    also reads the next ring slot (producer progress first, then 8 T' and the
+    2 words of top-string bytes) and the consumer's progress.
+Memory items "float": they fill whatever gap slots the arithmetic leaves,
+within a window of steps.  No scalar memory op is issued in the chunk loop, so
+lgkmcnt is exact: the block's single wait is lgkmcnt(K) with K = the LDS ops
+issued after its last read (the ledger in resolve_waits), never a wait for
+the writes behind them.
 
 Register roles are fixed so that nothing is copied between chunks: G'_6 and
 G'_7 are written into the carried operands gp6 / gin, the code word of the
 chunk grows in accp (the previous chunk's word is finished at step 0 and
-copied to acc), tm takes T'_7 for the next chunk.
+copied to acc), tm takes T'_7 for the next chunk.  The caller alternates the
+t / n (this / next ring slot) arrays.
 
 One block = N steps (1..8).  NEXT: a chunk followed by another one (N = 8):
-it also prepares sub for the next chunk's step 0 and computes H of its own
-last column.  Otherwise the flush block finishes the last column's code and
-score (the stripe's last column has no next step).
-
-The block also does the chunk's memory traffic in the gaps: G'_s of every
-lane goes to the LDS ring (only lane 63's address is the real slot; the
-others write a dummy) and H_s to the score tile, one coalesced 256-byte
-global_store_dword per column (column-major stripe tiles).  Nothing waits
-on these inside the block; the caller's lgkmcnt/vmcnt waits cover them.
+it reads the next slot, computes H of its own last column and advances the
+carried offsets.  Otherwise the flush block finishes the last column's code
+and score (the stripe's last column has no next step) and publishes it.
 
 Templates: chunk_asm<SH, SD, ST, N, NEXT> / flush_asm<SH, SD, ST, N> with
 SH = store scores, SD = direction codes, ST = stats (codes + |H| max).
 """
+import argparse
 import os
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 OUT = os.path.join(ROOT, "needleman-wunsch_amd", "csrc", "nw_chunk.inc")
+READ_STEP = 2          # first step whose gaps may issue the next slot's reads
+STORE = "normal"       # score stores: normal | nt (streaming hint) | fixed (diagnostic: one address)
 
 
 def gname(s):
     """Register of G'_s (s = -1, -2: the previous chunk's last two columns)."""
     return {-2: "gp6", -1: "gin", 6: "gp6", 7: "gin"}.get(s, f"g{s}")
+
+
+def shreg(s):
+    """Register of sh_s = wave_shr1(G'_{s-1}) with T'_{s-1} in lane 0: the DPP
+    leaves lane 0 (no source lane) at the register's old value, so it is
+    pre-filled with T'_{s-1} (tm: the previous chunk's T'_7; the others by a
+    v_mov scheduled into a free gap slot).  Three rotate, so the pre-fill of
+    step s can go anywhere in steps s-2 .. s-1."""
+    return "tm" if s == 0 else f"sh{s % 3}"
 
 
 def dg_reg(s):
@@ -58,92 +81,108 @@ def sub_reg(s):
     return "subA" if s % 2 == 0 else "subB"
 
 
-def byte_src(s):
-    """(sgpr operand, bfe offset) of the character of step s (s == 8: next chunk's byte 0)."""
-    if s == 8:
-        return "chn", 0
-    return ("chlo", 8 * s) if s < 4 else ("chhi", 8 * (s - 4))
+class Item:
+    """One filler instruction: name, text, dependencies, needs sh_s, LDS op, step window."""
+
+    def __init__(self, name, text, deps=(), needs_sh=False, lds=False, lo=0, hi=99):
+        self.name, self.text, self.deps, self.needs_sh = name, text, list(deps), needs_sh
+        self.lds, self.lo, self.hi = lds, lo, hi
 
 
-CODES = "align"    # or "cmp" (v_cmp + v_addc, the previous scheme; A/B runs)
-
-
-def code_items_cmp(s, sh):
-    """Flags of column s-1 via v_cmp -> SGPR mask -> v_addc shift-in (A/B reference)."""
-    Gp, Gpp, DGp = gname(s - 1), gname(s - 2), dg_reg(s - 1)
-    fresh = "0, 0" if s == 1 else "%[accp], %[accp]"
-    items = [("L", f"v_cmp_eq_i32_e64 %[sL], %[{Gp}], %[{Gpp}]", [], False),
-             ("D", f"v_cmp_eq_i32_e64 %[sD], %[{Gp}], %[{DGp}]", [], False),
-             ("U", f"v_cmp_eq_i32_e64 %[sU], %[{Gp}], %[{sh}]", [], True),
-             ("b1", f"v_addc_co_u32_e64 %[accp], vcc, {fresh}, %[sL]", ["L"], False),
-             ("b2", "v_addc_co_u32_e64 %[accp], vcc, %[accp], %[accp], %[sU]", ["U", "b1"], True),
-             ("b3", "v_addc_co_u32_e64 %[accp], vcc, %[accp], %[accp], %[sD]", ["D", "b2"], True),
-             ("G1", "s_nop 0", [], False)]
-    if s == 0:
-        items.append(("MV", "v_mov_b32_e32 %[acc], %[accp]", ["b3"], True))
-    return items
-
-
-def code_items(s, sh):
+def code_items(s, sh, SD):
     """Flags of column s-1 (sh = register holding wave_shr1 of G'_{s-1}) into its word.
 
     Every candidate X is <= G'_{s-1} (it is a max over them), so X == G' exactly
     when (G' - 1) - X < 0: the flag is the sign bit of one cheap VOP2
     subtraction, shifted into the word by v_alignbit_b32 (acc << 1 | d >> 31).
     Neighbouring scores differ by a few |m|+|k|+|d|, so the subtraction cannot
-    wrap.  No compares, no SGPR masks.
+    wrap.
     """
-    if CODES == "cmp":
-        return code_items_cmp(s, sh)
     Gp, Gpp, DGp = gname(s - 1), gname(s - 2), dg_reg(s - 1)
     hi = "0" if s == 1 else "%[accp]"      # first code of this chunk's word starts from 0
-    items = [("G1", f"v_add_u32_e32 %[gm1], -1, %[{Gp}]", [], False),
-             ("L", f"v_sub_u32_e32 %[dL], %[gm1], %[{Gpp}]", ["G1"], False),
-             ("D", f"v_sub_u32_e32 %[dD], %[gm1], %[{DGp}]", ["G1"], False),
-             ("U", f"v_sub_u32_e32 %[dU], %[gm1], %[{sh}]", ["G1"], True),
-             ("b1", f"v_alignbit_b32 %[accp], {hi}, %[dL], 31", ["L"], False),
-             ("b2", "v_alignbit_b32 %[accp], %[accp], %[dU], 31", ["U", "b1"], True),
-             ("b3", "v_alignbit_b32 %[accp], %[accp], %[dD], 31", ["D", "b2"], True)]
-    if s == 0:                # the previous chunk's word is complete: hand it out
-        items.append(("MV", "v_mov_b32_e32 %[acc], %[accp]", ["b3"], True))
+    items = [Item("G1", f"v_add_u32_e32 %[gm1], -1, %[{Gp}]"),
+             Item("L", f"v_sub_u32_e32 %[dL], %[gm1], %[{Gpp}]", ["G1"]),
+             Item("D", f"v_sub_u32_e32 %[dD], %[gm1], %[{DGp}]", ["G1"]),
+             Item("U", f"v_sub_u32_e32 %[dU], %[gm1], %[{sh}]", ["G1"], True),
+             Item("b1", f"v_alignbit_b32 %[accp], {hi}, %[dL], 31", ["L"]),
+             Item("b2", "v_alignbit_b32 %[accp], %[accp], %[dU], 31", ["U", "b1"], True),
+             Item("b3", "v_alignbit_b32 %[accp], %[accp], %[dD], 31", ["D", "b2"], True)]
+    if s == 0:                # the previous chunk's word is complete: hand it out (and store it)
+        items.append(Item("MV", "v_mov_b32_e32 %[acc], %[accp]", ["b3"], True))
+        if SD:                # (chunk 0 stores its garbage word into the stripe's pad row)
+            items.append(Item("CS", "global_store_dword %[dv], %[acc], %[db]", ["MV"], True))
+            items.append(Item("CV", "v_add_u32_e32 %[dv], 0x100, %[dv]", ["CS"], True))
     return items
 
 
-def score_items(s, A, S=False):
-    """H (and |H| max, and its store) of column s-1."""
+def score_items(s, A, S):
+    """H (and its store, and |H| max) of column s-1."""
     h = f"h{s - 1}"
-    items = [("H", f"v_add3_u32 %[{h}], %[{gname(s - 1)}], %[nlo], %[k{s - 1}]", [], False)]
+    items = [Item("H", f"v_add3_u32 %[{h}], %[{gname(s - 1)}], %[nlo], %[k{s - 1}]")]
     if S:
-        items.append(("ST", f"global_store_dword %[hv], %[{h}], %[hb] offset:{256 * (s - 1)}", ["H"], False))
+        off = 0 if STORE == "fixed" else 256 * (s - 1)
+        hint = " nt" if STORE == "nt" else ""
+        items.append(Item("ST", f"global_store_dword %[hv], %[{h}], %[hb] offset:{off}{hint}", ["H"]))
     if A:
-        items.append(("A1", f"v_sub_u32_e32 %[tmp], 0, %[{h}]", ["H"], False))
-        items.append(("A2", f"v_max3_i32 %[gav], %[gav], %[{h}], %[tmp]", ["A1"], False))
+        items.append(Item("A1", f"v_sub_u32_e32 %[tmp], 0, %[{h}]", ["H"]))
+        items.append(Item("A2", f"v_max3_i32 %[gav], %[gav], %[{h}], %[tmp]", ["A1"]))
     return items
 
 
 def ring_item(s):
     """G'_{s-1} of every lane to the ring (lane 63: the slot)."""
-    return ("R", f"ds_write_b32 %[ra], %[{gname(s - 1)}] offset:{4 * (s - 1)}", [], False)
+    return Item("R", f"ds_write_b32 %[ra], %[{gname(s - 1)}] offset:{4 * (s - 1)}", lds=True)
 
 
-def step(s, N, F, H, A, nxt, S=False):
+def sub_items(b):
+    """sub' of column b of this chunk: byte compare of top-string byte b + select."""
+    src, sel = ("t8", b) if b < 4 else ("t9", b - 4)
+    return [Item("M", f"v_cmp_eq_u32_sdwa vcc, %[{src}], %[c2] src0_sel:BYTE_{sel} src1_sel:DWORD"),
+            Item("X", f"v_cndmask_b32_e64 %[{sub_reg(b)}], %[vck], %[vcm], vcc", ["M"])]
+
+
+def floating_items(N, nxt):
+    """Memory items with a window of steps [lo, hi]; issued in list order.
+
+    Ring counters: cb = &ctr[2w], ctr[2v+2] = prog[v] (chunks in wave v's ring),
+    ctr[2v+3] = cons[v+1] (chunks wave v+1 took), so this wave's producer
+    progress and consumer progress are one 8-byte pair at cb+8, its own cons at
+    cb+4 and the prog of the wave below at cb+16.
+    """
+    last = N - 1
+    its = [Item(f"SH{s}", f"v_mov_b32_e32 %[{shreg(s)}], %[t{s - 1}]", lo=max(s - 2, 0), hi=s - 1)
+           for s in range(1, N)]
+    its += [Item("CW", "ds_write_b32 %[cb], %[cv] offset:4", lds=True, hi=last),  # ring slot taken
+           Item("W8", "ds_write_b32 %[ra], %[t8] offset:32", lds=True, hi=last),  # top-string bytes
+           Item("W9", "ds_write_b32 %[ra], %[t9] offset:36", lds=True, hi=last)]  # go down the ring
+    if nxt:
+        # the next chunk's slot: progress first (slot data read after a
+        # progress value that covers it is valid), then T' and the bytes
+        # (deadline step 5: the block's final wait finds them done)
+        lo, hi = READ_STEP, min(READ_STEP + 3, last)
+        its.append(Item("PQ", "ds_read_b64 %[pq], %[cb] offset:8", lds=True, lo=lo, hi=hi))
+        its.append(Item("TA", "ds_read_b128 %[nA], %[rd]", lds=True, lo=lo, hi=hi))
+        its.append(Item("TB", "ds_read_b128 %[nB], %[rd] offset:16", lds=True, lo=lo, hi=hi))
+        its.append(Item("CC", "ds_read_b64 %[nC], %[rd] offset:32", lds=True, lo=lo, hi=hi))
+        # tm (sh_0's register) is free after step 0: T'_7 for the next chunk
+        its.append(Item("TM", "v_mov_b32_e32 %[tm], %[t7]", lo=1, hi=last))
+    return its
+
+
+def step(s, N, F, H, A, S, SD, nxt, floating):
     Gp = gname(s - 1)
-    Tm = "tm" if s == 0 else f"t{s - 1}"
+    Tm = shreg(s)
     fill = []
+    if s == 0:
+        fill += sub_items(0)            # first gap: sub' of this step itself
     if F:
-        fill += code_items(s, Tm)
+        fill += code_items(s, Tm, SD)
     if s > 0:
         fill.append(ring_item(s))
     if H and s > 0:
         fill += score_items(s, A, S)
-    if s + 1 < N or nxt:
-        src, off = byte_src(s + 1)
-        bfe = f"s_bfe_u32 %[sC], %[{src}], {hex(off | (8 << 16))}" if off else f"s_and_b32 %[sC], %[{src}], 0xff"
-        fill.append(("S", bfe, [], False))
-        fill.append(("M", "v_cmp_eq_u32_e64 %[sM], %[sC], %[c2]", ["S"], False))
-        fill.append(("X", f"v_cndmask_b32_e64 %[{sub_reg(s + 1)}], %[vck], %[vcm], %[sM]", ["M"], False))
-    if s == 7 and nxt:
-        fill.append(("TM", "v_mov_b32_e32 %[tm], %[t7]", [], False))
+    if s + 1 < N:
+        fill += sub_items(s + 1)
     chain_head = [
         f"v_mov_b32_dpp %[{Tm}], %[{Gp}] wave_shr:1 row_mask:0xf bank_mask:0xf",
         f"v_add_u32_e32 %[{dg_reg(s)}], %[{Tm}], %[{sub_reg(s)}]",
@@ -157,63 +196,98 @@ def step(s, N, F, H, A, nxt, S=False):
 
     def take(allow_sh, k=2):
         got = []
+        names = lambda: [g.name for g in got]
         for it in list(pending):
             if len(got) == k:
                 break
-            name, text, deps, needs_sh = it
-            if needs_sh and not allow_sh:
+            if it.needs_sh and not allow_sh:
                 continue
-            if all(dd in done or dd in [g[0] for g in got] for dd in deps):
+            if all(dd in done or dd in names() for dd in it.deps):
                 got.append(it)
                 pending.remove(it)
+        while len(got) < k:               # earliest deadline first; reads keep their order
+            ok = [f for f in floating if f.lo <= s]
+            if not ok:
+                break
+            f = min(ok, key=lambda f: f.hi)
+            floating.remove(f)
+            got.append(f)
         for g in got:
-            done.add(g[0])
-        return [g[1] for g in got]
+            done.add(g.name)
+        return got
 
     def gap(allow_sh):
         got = take(allow_sh)
-        if len(got) == 2:
-            out.extend(got)
-        elif len(got) == 1:
-            out.extend(got + ["s_nop 0"])
-        else:
-            out.append("s_nop 1")
+        out.extend(got)
+        if len(got) == 1:
+            out.append(Item("", "s_nop 0"))
+        elif not got:
+            out.append(Item("", "s_nop 1"))
 
     gap(False)                     # before the DPP shift of G'_{s-1}
-    out.extend(chain_head)
+    out.extend(Item("", t) for t in chain_head)
     g = gname(s)
     for dp in dpps:
         gap(True)                  # before each DPP max reading the previous VALU result
-        out.append(f"v_max_i32_dpp %[{g}], %[{g}], %[{g}] {dp} bank_mask:0xf")
+        out.append(Item("", f"v_max_i32_dpp %[{g}], %[{g}], %[{g}] {dp} bank_mask:0xf"))
     while pending:                 # anything left runs after the scan
         got = take(True, 1)
-        assert got, pending
+        assert got, [p.name for p in pending]
         out.extend(got)
+    for f in [f for f in floating if f.hi <= s]:
+        floating.remove(f)
+        out.append(f)
     return out
 
 
-def block(N, F, H, A, nxt, S):
-    lines = []
+def resolve_waits(items):
+    """Turn s_waitcnt lgkmcnt(@X) into the count of LDS ops issued after the LDS op X."""
+    text = []
+    for i, it in enumerate(items):
+        t = it.text
+        if "@" in t:
+            tag = t[t.index("@") + 1:t.index(")")]
+            pos = [j for j, x in enumerate(items[:i]) if x.name == tag and x.lds]
+            assert pos, tag
+            after = sum(1 for x in items[pos[-1] + 1:i] if x.lds)
+            t = t.replace("@" + tag, str(min(after, 15)))
+        text.append(t)
+    return text
+
+
+def block(N, F, H, A, S, SD, nxt):
+    items = []
+    floating = floating_items(N, nxt)
     for s in range(N):
-        lines += step(s, N, F, H, A, nxt, S)
+        items += step(s, N, F, H, A, S, SD, nxt, floating)
+    assert not floating, [f.name for f in floating]
     if nxt:                        # the chunk's last column (G'_7 is final now)
-        lines.append(ring_item(8)[1])
+        items.append(ring_item(8))
         if H:
-            lines += [t for _, t, _, _ in score_items(8, A, S)]
-    return lines
+            items += score_items(8, A, S)
+        items.append(Item("PW", "ds_write_b32 %[cb], %[cv] offset:16", lds=True))   # wave below may go
+        items.append(Item("CA", "v_add_u32_e32 %[cv], 1, %[cv]"))
+        if STORE != "fixed":
+            items.append(Item("HA", "v_add_u32_e32 %[hv], 0x800, %[hv]"))
+        items.append(Item("NA", "v_subrev_u32_e32 %[nlo], %[d8], %[nlo]"))
+        last_read = [it.name for it in items if it.lds and it.text.startswith("ds_read")][-1]
+        items.append(Item("WE", f"s_waitcnt lgkmcnt(@{last_read})"))   # progress and the next slot are in
+    return resolve_waits(items)
 
 
 def flush(N, F, H, A, S):
-    """Code, ring entry and score of the block's last column s = N-1 (no next step)."""
+    """Code, ring entry and score of the block's last column s = N-1; then the wave below may go."""
     s = N
-    out = [ring_item(s)[1]]
+    out = [ring_item(s).text]
     if F:
-        items = {n: t for n, t, _, _ in code_items(s, f"t{s - 1}")}
-        out += [items["G1"], items["L"], items["D"],
-                f"v_mov_b32_dpp %[t{s - 1}], %[{gname(s - 1)}] wave_shr:1 row_mask:0xf bank_mask:0xf",
+        sh = shreg(s)
+        items = {it.name: it.text for it in code_items(s, sh, False)}
+        out += [f"v_mov_b32_e32 %[{sh}], %[t{s - 1}]", items["G1"], items["L"], items["D"],
+                f"v_mov_b32_dpp %[{sh}], %[{gname(s - 1)}] wave_shr:1 row_mask:0xf bank_mask:0xf",
                 items["U"], items["b1"], items["b2"], items["b3"]]
     if H:
-        out += [t for _, t, _, _ in score_items(s, A, S)]
+        out += [it.text for it in score_items(s, A, S)]
+    out.append("ds_write_b32 %[cb], %[cv] offset:16")
     return out
 
 
@@ -221,19 +295,21 @@ OPERANDS = r'''
 #define NW_CHUNK_OPERANDS                                                                                  \
     : [g0] "=&v"(r.g[0]), [g1] "=&v"(r.g[1]), [g2] "=&v"(r.g[2]), [g3] "=&v"(r.g[3]),                      \
       [g4] "=&v"(r.g[4]), [g5] "=&v"(r.g[5]), [gp6] "+v"(r.gp6), [gin] "+v"(r.gin),                       \
-      [t0] "+v"(r.t[0]), [t1] "+v"(r.t[1]), [t2] "+v"(r.t[2]), [t3] "+v"(r.t[3]),                          \
-      [t4] "+v"(r.t[4]), [t5] "+v"(r.t[5]), [t6] "+v"(r.t[6]), [t7] "+v"(r.t[7]),                          \
+      [sh0] "=&v"(sh0_), [sh1] "=&v"(sh1_), [sh2] "=&v"(sh2_),                                             \
+      [nA] "=&v"(ns.a), [nB] "=&v"(ns.b), [nC] "=&v"(ns.c), [pq] "=&v"(r.pq),                              \
       [tm] "+v"(r.tm), [dgA] "+v"(r.dgA), [dgB] "+v"(r.dgB), [subA] "+v"(r.subA), [subB] "+v"(r.subB),     \
       [h0] "=&v"(r.h[0]), [h1] "=&v"(r.h[1]), [h2] "=&v"(r.h[2]), [h3] "=&v"(r.h[3]),                      \
       [h4] "=&v"(r.h[4]), [h5] "=&v"(r.h[5]), [h6] "=&v"(r.h[6]), [h7] "=&v"(r.h[7]),                      \
       [accp] "+v"(r.accp), [acc] "=&v"(r.acc), [gav] "+v"(r.gav), [tmp] "=&v"(tmp_),                      \
-      [gm1] "=&v"(gm1_), [dL] "=&v"(dL_), [dU] "=&v"(dU_), [dD] "=&v"(dD_), [sM] "=&s"(sM_), [sC] "=&s"(sC_), \
-      [sL] "=&s"(sL_), [sU] "=&s"(sU_), [sD] "=&s"(sD_)                                                  \
-    : [c2] "v"(k.c2), [vcm] "v"(k.vcm), [vck] "v"(k.vck), [nlo] "v"(k.nlo),                               \
-      [chlo] "s"(ch.lo), [chhi] "s"(ch.hi), [chn] "s"(ch.nlo),                                            \
+      [gm1] "=&v"(gm1_), [dL] "=&v"(dL_), [dU] "=&v"(dU_), [dD] "=&v"(dD_),                                \
+      [cv] "+v"(r.cv), [hv] "+v"(r.hv), [dv] "+v"(r.dv),         \
+      [nlo] "+v"(r.nlo)                                                                                    \
+    : [t0] "v"(ts.a[0]), [t1] "v"(ts.a[1]), [t2] "v"(ts.a[2]), [t3] "v"(ts.a[3]),                          \
+      [t4] "v"(ts.b[0]), [t5] "v"(ts.b[1]), [t6] "v"(ts.b[2]), [t7] "v"(ts.b[3]), [t8] "v"(ts.c[0]),         \
+      [t9] "v"(ts.c[1]), [c2] "v"(k.c2), [vcm] "v"(k.vcm), [vck] "v"(k.vck), [d8] "s"(k.d8),                                \
       [k0] "v"(k.kd[0]), [k1] "v"(k.kd[1]), [k2] "v"(k.kd[2]), [k3] "v"(k.kd[3]),                          \
       [k4] "v"(k.kd[4]), [k5] "v"(k.kd[5]), [k6] "v"(k.kd[6]), [k7] "v"(k.kd[7]),                          \
-      [ra] "v"(ra), [hv] "v"(k.hv), [hb] "s"(hb)
+      [ra] "v"(ra), [rd] "v"(rd), [cb] "v"(k.cb), [hb] "s"(k.hb), [db] "s"(k.db)
 '''
 # The flush reads values the chunk block produced: every value operand is read-write.
 FLUSH_OPERANDS = (OPERANDS.replace("NW_CHUNK_OPERANDS", "NW_FLUSH_OPERANDS")
@@ -250,21 +326,22 @@ def tf(b):
 
 
 def main():
-    global OUT, CODES
-    import argparse
+    global OUT, READ_STEP, STORE
     ap = argparse.ArgumentParser()
-    ap.add_argument("--codes", choices=("align", "cmp"), default="align")
     ap.add_argument("--out", default=OUT)
+    ap.add_argument("--read-step", type=int, default=READ_STEP)
+    ap.add_argument("--store", choices=("normal", "nt", "fixed"), default=STORE)
     args = ap.parse_args()
-    OUT, CODES = args.out, args.codes
+    OUT, READ_STEP, STORE = args.out, args.read_step, args.store
     parts = ["// GENERATED by tools/gen_chunk_asm.py -- do not edit; see the generator for the schedule.\n",
              OPERANDS, FLUSH_OPERANDS,
              "template <bool SH, bool SD, bool ST, int N, bool NEXT>\n"
-             "__device__ __forceinline__ void chunk_asm(ChunkRegs& r, const ChunkConst& k, const ChunkChars& ch,\n"
-             "                                          int ra, const int32_t* hb);\n"
+             "__device__ __forceinline__ void chunk_asm(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts,\n"
+             "                                          RingSlot& ns, int ra, int rd);\n"
              "template <bool SH, bool SD, bool ST, int N>\n"
-             "__device__ __forceinline__ void flush_asm(ChunkRegs& r, const ChunkConst& k, int ra, const int32_t* hb);\n"]
-    decl = "    int tmp_, gm1_, dL_, dU_, dD_; uint64_t sM_, sL_, sU_, sD_; uint32_t sC_;\n"
+             "__device__ __forceinline__ void flush_asm(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts, int ra);\n"]
+    decl = "    int tmp_, gm1_, dL_, dU_, dD_, sh0_, sh1_, sh2_;\n"
+    unpack = ""
     for SH in (0, 1):
         for SD in (0, 1):
             for ST in (0, 1):
@@ -274,13 +351,13 @@ def main():
                     for nxt in ((0, 1) if N == 8 else (0,)):
                         parts.append(
                             f"template <> __device__ __forceinline__ void chunk_asm<{head}, {N}, {tf(nxt)}>"
-                            f"(ChunkRegs& r, const ChunkConst& k, const ChunkChars& ch, int ra, const int32_t* hb) {{\n"
-                            f"{decl}    asm volatile(\n{cstr(block(N, F, H, A, nxt, S))}\n"
+                            f"(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts, RingSlot& ns, int ra, int rd) {{\n"
+                            f"{decl}{unpack}    asm volatile(\n{cstr(block(N, F, H, A, S, SD, nxt))}\n"
                             f"        NW_CHUNK_OPERANDS : \"vcc\", \"scc\", \"memory\");\n}}\n")
                     parts.append(
                         f"template <> __device__ __forceinline__ void flush_asm<{head}, {N}>"
-                        f"(ChunkRegs& r, const ChunkConst& k, int ra, const int32_t* hb) {{\n{decl}"
-                        f"    const ChunkChars ch{{0u, 0u, 0u}};\n"
+                        f"(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts, int ra) {{\n{decl}"
+                        f"    RingSlot ns;\n    const int rd = 0;\n"
                         f"    asm volatile(\n{cstr(flush(N, F, H, A, S))}\n"
                         f"        NW_FLUSH_OPERANDS : \"vcc\", \"scc\", \"memory\");\n}}\n")
     parts.append("#undef NW_CHUNK_OPERANDS\n#undef NW_FLUSH_OPERANDS\n")
