@@ -90,15 +90,17 @@ int nw_fill(const char *s1, int64_t L1, const char *s2, int64_t L2,
  * Device-resident table (the 100k x 100k path: the 45 GB table stays in HBM).
  *
  * Device layout (DESIGN.md "Data layout in HBM"):
- *   scores: column-major stripe tiles.  Row 0 and column 0 (the seeds
- *           -i*d, -j*d) are not stored.  Interior cell (i, j) has stripe
- *           g = (j-1)/64, lane l = (j-1)%64 and is element
- *           g*P + (i-1)*64 + l with P = nw_table_score_pitch() = 512*NQ:
- *           one column of one stripe is 256 contiguous bytes.
+ *   scores: stripe quad tiles.  Row 0 and column 0 (the seeds -i*d,
+ *           -j*d) are not stored.  Interior cell (i, j) has stripe
+ *           g = (j-1)/64, lane l = (j-1)%64, quad u = (i-1)/4, r = (i-1)%4
+ *           and is element g*P + (u*64 + l)*4 + r with
+ *           P = nw_table_score_pitch() = 512*NQ: a lane's 4 consecutive
+ *           columns are 16 contiguous bytes, 8 columns of a stripe 2 KB.
  *   dirs  : 32-bit words, one per (64-row stripe g, 8-column group q, lane l):
- *           word (g*NQ + q)*64 + l, NQ = ceil(L1/8), holds the codes of cells
- *           (i = 8q+1+s, j = 64g+1+l), s = 0..7, 3 bits each: code s in bits
- *           [21-3s, 23-3s] (bits 24..31 are 0).
+ *           word (g*(NQ+1) + q + 1)*64 + l, NQ = ceil(L1/8) (row 0 of each
+ *           stripe is padding), holds the codes of cells (i = 8q+1+s,
+ *           j = 64g+1+l), s = 0..7, 3 bits each: code s in bits [21-3s, 23-3s]
+ *           (bits 24..31 are 0).
  */
 typedef struct nw_table nw_table;
 

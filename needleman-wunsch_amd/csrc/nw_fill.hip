@@ -42,6 +42,9 @@
 namespace {
 
 constexpr int CH = 8;                 // columns per chunk (= codes per dirs word)
+#ifndef NW_XCD_DEFAULT
+#define NW_XCD_DEFAULT 0
+#endif
 constexpr int64_t SPIN_TICKS = 200000000;  // 2 s of s_memrealtime (100 MHz)
 // Panel boundary granule tags: the fill's epoch (1 .. 2^31-1), or the epoch
 // with bit 31 set when the panel above failed that fill (per-epoch, so a stale
@@ -78,6 +81,7 @@ struct FillArgs {
     uint64_t* xout;         // bottom row granules for the panel below, or null
     uint32_t* xflag;        // host-visible: xflag[b] = epoch once block b of xout is written
     int32_t xblk;           // chunks per block
+    int32_t xcd_map;        // 1: one WG-stripe per block, consecutive WG-stripes on blocks of one XCD
 };
 
 // ---------------------------------------------------------------- DPP helpers
@@ -171,7 +175,7 @@ __device__ __forceinline__ int run_last(ChunkRegs& r, const ChunkConst& k, const
     RingSlot n;
     chunk_asm<SH, SD, ST, N, false>(r, k, t, n, ra, 0);
     flush_asm<SH, SD, ST, N>(r, k, t, ra);
-    if constexpr (SH || ST) return r.h[N - 1];
+    if constexpr ((SH && !NW_SCORE_X4) || ST) return r.h[N - 1];
     else return g_of(r, N - 1) + r.nlo + k.kd[N - 1];
 }
 template <bool SH, bool SD, bool ST>
@@ -205,6 +209,27 @@ __device__ __forceinline__ uint64_t read_slot(int cb, int rd, RingSlot& s) {
         : "memory");
     return pq;
 }
+
+#if NW_SCORE_X4
+// Scores of one chunk from C++ (H = G' + nlo + kd, 8 v_add3): two 16-byte
+// stores per lane into the quad tile (see score_index), 2 KB per wave.
+__device__ __forceinline__ void store_chunk_scores(const ChunkRegs& r, const ChunkConst& k, int nl, bool have_h) {
+    v4i qa, qb;
+    if (have_h) {
+        qa = v4i{r.h[0], r.h[1], r.h[2], r.h[3]};
+        qb = v4i{r.h[4], r.h[5], r.h[6], r.h[7]};
+    } else {
+        qa = v4i{r.g[0] + nl + k.kd[0], r.g[1] + nl + k.kd[1], r.g[2] + nl + k.kd[2], r.g[3] + nl + k.kd[3]};
+        qb = v4i{r.g[4] + nl + k.kd[4], r.g[5] + nl + k.kd[5], r.gp6 + nl + k.kd[6], r.gin + nl + k.kd[7]};
+    }
+    asm volatile(
+        "global_store_dwordx4 %[hv], %[qa], %[hb]" NW_SCORE_HINT "\n\t"
+        "global_store_dwordx4 %[hv], %[qb], %[hb] offset:1024" NW_SCORE_HINT
+        :
+        : [hv] "v"(r.hv), [qa] "v"(qa), [qb] "v"(qb), [hb] "s"(k.hb)
+        : "memory");
+}
+#endif
 
 // Hand-off granule load: agent scope between workgroups of one fill, system
 // scope (bypassing L2) for the panel boundary, which another agent writes.
@@ -253,6 +278,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
     __shared__ __attribute__((aligned(8))) int ctr[2 * W + 4];
     __shared__ int sh_sidx;
     __shared__ int sh_abort;
+    __shared__ int sh_done;     // XCD map: this block's one WG-stripe is taken
 
     const int lane = threadIdx.x & 63;
     const int w = uni(threadIdx.x >> 6);
@@ -262,10 +288,19 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
     int vck = 2 * a.d - a.k;
     const int NC = a.NC;
     const int nlast = a.L1 - CH * (NC - 1);   // steps in the last chunk (1..8)
+    if (threadIdx.x == 0) sh_done = 0;
 
     for (;;) {
         if (threadIdx.x == 0) {
-            const int sidx = (int)atomicAdd(&a.ctl[CTL_NEXT], 1u);
+            // XCD map: blocks b and b+8 share an XCD (and its L2), so block
+            // b takes WG-stripe (b%8)*q + min(b%8, r) + b/8 (grid = 8q + r):
+            // the hand-offs between consecutive WG-stripes stay inside one
+            // L2 except at 7 group boundaries.  Every block holds exactly
+            // one WG-stripe and waits only on a block that holds another.
+            const int b = blockIdx.x, q = gridDim.x / 8, rr = gridDim.x % 8;
+            const int sidx = a.xcd_map ? (sh_done ? a.NSW : (b % 8) * q + min(b % 8, rr) + b / 8)
+                                       : (int)atomicAdd(&a.ctl[CTL_NEXT], 1u);
+            sh_done = 1;
             sh_sidx = sidx;
             sh_abort = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - (sidx * a.SQ + min(sidx, a.SR)));
@@ -393,7 +428,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             r.gav = 0;
             r.pq = 0;
             r.cv = 1;
-            r.hv = lane * 4;
+            r.hv = NW_SCORE_X4 ? lane * 16 : lane * 4;
             r.dv = lane * 4;
             r.nlo = -(64 * w + lane) * d;
             // Ring writes: lane 63 into the slot, the other lanes into a
@@ -478,7 +513,16 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             auto full_chunk = [&](int c, auto slotc, const RingSlot& cur, RingSlot& nxt) -> bool {
                 constexpr int Q = decltype(slotc)::value;
                 constexpr int NQ = (Q + 1) % R;
+#if NW_SCORE_X4
+                const int nl = r.nlo;
+#endif
                 chunk_asm<SH, SD, ST, 8, true>(r, kc, cur, nxt, ra[Q], rd[NQ]);
+#if NW_SCORE_X4
+                if (SH) {
+                    store_chunk_scores(r, kc, nl, ST);
+                    r.hv += CH * 64 * 4;
+                }
+#endif
                 after_chunk(c, Q, CH, false);
                 // (wave-uniform: every lane read the same counters)
                 if (uni((int)(uint32_t)r.pq) > c + 1 && uni((int)(r.pq >> 32)) >= c + 2 - R) return true;
@@ -509,7 +553,14 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             if (!aborted && wait_slot(c, lds_addr(tin) + (c % R) * SLOT * 4, tA)) {
                 rebase(c);
                 const int slot = c % R;
+#if NW_SCORE_X4
+                const int nl = r.nlo;
+#endif
                 const int hl = run_last_n<SH, SD, ST>(nlast, r, kc, tA, ring0 + slot * SLOT * 4);
+#if NW_SCORE_X4
+                // (columns past the last one land in the tile's own padding)
+                if (SH) store_chunk_scores(r, kc, nl, ST);
+#endif
                 if (!SH) a.lastcol[j0 + lane] = hl;   // score-only: H[L1][*]
                 after_chunk(c, slot, nlast, true);
             }
@@ -558,16 +609,23 @@ struct TableView {
 // Score of cell (i, j) in the device layout.  Row 0 and column 0 are the
 // reference's seeds (computation.c:93-120), computed, not stored; a panel's
 // row 0 is the last row of the panel above, kept in its xin granules.
-// Interior cells live in column-major stripe tiles: stripe g = (j-1)/64,
-// lane l = (j-1)%64, column i at
-//     g*spitch + (i-1)*64 + l,   spitch = 512*NC,
-// i.e. one column of one stripe is 256 contiguous bytes (one coalesced
-// store per column step of the fill).
+// Interior cells live in stripe tiles: stripe g = (j-1)/64, lane l =
+// (j-1)%64, spitch = 512*NC elements per stripe.  Quad tiles (NW_SCORE_X4):
+// column i = 4q + r + 1 at g*spitch + (q*64 + l)*4 + r, so a lane's 4
+// consecutive columns are one 16-byte store and a chunk is 2 KB contiguous.
+// Column tiles: g*spitch + (i-1)*64 + l, one 256-byte store per column.
+__host__ __device__ __forceinline__ int64_t score_index(int64_t r, int64_t c, int64_t spitch) {
+#if NW_SCORE_X4
+    return (r >> 6) * spitch + ((c >> 2) * 64 + (r & 63)) * 4 + (c & 3);
+#else
+    return (r >> 6) * spitch + c * 64 + (r & 63);
+#endif
+}
+
 __device__ __forceinline__ int32_t score_at(const TableView& v, int64_t i, int64_t j) {
     if (i == 0) return (int32_t)(-(j + v.row_base) * (int64_t)v.d);
     if (j == 0) return v.top ? (int32_t)(uint32_t)v.top[i - 1] + v.d : (int32_t)(-i * (int64_t)v.d);
-    const int64_t r = j - 1, c = i - 1;
-    return v.tiles[(r >> 6) * v.spitch + c * 64 + (r & 63)];
+    return v.tiles[score_index(j - 1, i - 1, v.spitch)];
 }
 
 // Dense i-major copy of columns [i0, i1): out[(i-i0)*(L2+1) + j].
@@ -787,6 +845,13 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         // and of the transport (RCCL), which its hand-off waits on.
         const int per_cu = panel ? std::max(1, std::min(2, occ - 1)) : std::min(occ, 16);
         const int64_t grid = std::min<int64_t>(a.NSW, (int64_t)t->ncu * per_cu);
+        // One WG-stripe per block when the grid covers them all (a plain fill
+        // with all blocks resident); panels keep the dequeue (their
+        // neighbours' kernels share the CUs).
+        {
+            const char* e = getenv("NW_XCD");
+            a.xcd_map = (!panel && grid == a.NSW && (e ? atoi(e) != 0 : NW_XCD_DEFAULT)) ? 1 : 0;
+        }
         a.nslot = (int32_t)std::min<int64_t>(grid + 1, (int64_t)(t->gran_bytes / 8 / a.gpitch));
         if (a.nslot < grid + 1) return fail(NW_ERR_ARG, "nw_table_fill: granule buffer too small");
         if (a.NSW > 1) NW_HIPCHK(hipMemsetAsync(t->gran, 0, (size_t)a.nslot * a.gpitch * 8, t->stream));
@@ -827,7 +892,7 @@ int fill_finish(nw_table* t) {
     int32_t corner = 0;
     if (L1 > 0 && L2 > 0) {
         const int64_t r = L2 - 1, q = L1 - 1;
-        const int32_t* src = sh ? t->H + (r >> 6) * t->spitch + q * 64 + (r & 63) : t->lastcol + L2;
+        const int32_t* src = sh ? t->H + score_index(r, q, t->spitch) : t->lastcol + L2;
         NW_HIPCHK(hipMemcpyAsync(&corner, src, 4, hipMemcpyDeviceToHost, t->stream));
     }
     NW_HIPCHK(hipStreamSynchronize(t->stream));

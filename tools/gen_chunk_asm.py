@@ -56,7 +56,9 @@ import os
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 OUT = os.path.join(ROOT, "needleman-wunsch_amd", "csrc", "nw_chunk.inc")
 READ_STEP = 2          # first step whose gaps may issue the next slot's reads
-STORE = "normal"       # score stores: normal | nt (streaming hint) | fixed (diagnostic: one address)
+STORE = "normal"       # score stores: normal | fixed (diagnostic: one address)
+STORE_HINT = "nt"      # cache-policy bits of the score stores (e.g. "nt", "sc1")
+SCORE_X4 = False       # scores leave as 2 x global_store_dwordx4 per chunk from C++ (quad tiles)
 
 
 def gname(s):
@@ -116,12 +118,18 @@ def code_items(s, sh, SD):
 
 
 def score_items(s, A, S):
-    """H (and its store, and |H| max) of column s-1."""
+    """H (and its store, and |H| max) of column s-1.  With SCORE_X4 the caller
+    computes and stores H (16 bytes per lane per 4 columns); the block only
+    needs H for the stats."""
+    if SCORE_X4:
+        S = False
+        if not A:
+            return []
     h = f"h{s - 1}"
     items = [Item("H", f"v_add3_u32 %[{h}], %[{gname(s - 1)}], %[nlo], %[k{s - 1}]")]
     if S:
         off = 0 if STORE == "fixed" else 256 * (s - 1)
-        hint = " nt" if STORE == "nt" else ""
+        hint = (" " + STORE_HINT) if STORE_HINT else ""
         items.append(Item("ST", f"global_store_dword %[hv], %[{h}], %[hb] offset:{off}{hint}", ["H"]))
     if A:
         items.append(Item("A1", f"v_sub_u32_e32 %[tmp], 0, %[{h}]", ["H"]))
@@ -257,6 +265,8 @@ def resolve_waits(items):
 
 def block(N, F, H, A, S, SD, nxt):
     items = []
+    if STORE == "fixed" and S and not SCORE_X4:     # diagnostic: every store to this lane's first word (hv = lane*4)
+        items.append(Item("HF", "v_and_b32_e32 %[hv], 0xff, %[hv]"))
     floating = floating_items(N, nxt)
     for s in range(N):
         items += step(s, N, F, H, A, S, SD, nxt, floating)
@@ -267,7 +277,7 @@ def block(N, F, H, A, S, SD, nxt):
             items += score_items(8, A, S)
         items.append(Item("PW", "ds_write_b32 %[cb], %[cv] offset:16", lds=True))   # wave below may go
         items.append(Item("CA", "v_add_u32_e32 %[cv], 1, %[cv]"))
-        if STORE != "fixed":
+        if STORE != "fixed" and S and not SCORE_X4:
             items.append(Item("HA", "v_add_u32_e32 %[hv], 0x800, %[hv]"))
         items.append(Item("NA", "v_subrev_u32_e32 %[nlo], %[d8], %[nlo]"))
         last_read = [it.name for it in items if it.lds and it.text.startswith("ds_read")][-1]
@@ -326,14 +336,18 @@ def tf(b):
 
 
 def main():
-    global OUT, READ_STEP, STORE
+    global OUT, READ_STEP, STORE, STORE_HINT, SCORE_X4
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=OUT)
     ap.add_argument("--read-step", type=int, default=READ_STEP)
-    ap.add_argument("--store", choices=("normal", "nt", "fixed"), default=STORE)
+    ap.add_argument("--store", choices=("normal", "fixed"), default=STORE)
+    ap.add_argument("--store-hint", default=STORE_HINT)
+    ap.add_argument("--x4", type=int, default=int(SCORE_X4))
     args = ap.parse_args()
-    OUT, READ_STEP, STORE = args.out, args.read_step, args.store
+    OUT, READ_STEP, STORE, STORE_HINT = args.out, args.read_step, args.store, args.store_hint
+    SCORE_X4 = bool(args.x4)
     parts = ["// GENERATED by tools/gen_chunk_asm.py -- do not edit; see the generator for the schedule.\n",
+             f"#define NW_SCORE_X4 {int(SCORE_X4)}\n#define NW_SCORE_HINT \"{(' ' + STORE_HINT) if STORE_HINT else ''}\"\n",
              OPERANDS, FLUSH_OPERANDS,
              "template <bool SH, bool SD, bool ST, int N, bool NEXT>\n"
              "__device__ __forceinline__ void chunk_asm(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts,\n"

@@ -46,6 +46,21 @@ __global__ void k(int* out, long long* cyc, int n) {
 #define I_SUB32(r) "v_sub_u32_e32 %" #r ", %" #r ", %0\n"
 #define I_DSW1(r) "ds_write_b32 %15, %" #r " offset:" #r "*4\n"
 #define I_SST(r) "s_store_dwordx2 %8, %14, " #r "*8\n"
+#define I_AND(r) "v_and_b32_e32 %" #r ", %0, %" #r "\n"
+#define I_XOR(r) "v_xor_b32_e32 %" #r ", %0, %" #r "\n"
+#define I_LSR(r) "v_lshrrev_b32_e32 %" #r ", 3, %" #r "\n"
+#define I_MOV(r) "v_mov_b32_e32 %" #r ", %0\n"
+#define I_ALIGN(r) "v_alignbit_b32 %" #r ", %" #r ", %0, 31\n"
+#define I_ADDSDWA(r) "v_add_u32_sdwa %" #r ", %" #r ", %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n"
+#define I_CMPSDWA(r) "v_cmp_eq_u32_sdwa vcc, %" #r ", %0 src0_sel:BYTE_1 src1_sel:DWORD\n"
+#define I_SUBREV(r) "v_subrev_u32_e32 %" #r ", %0, %" #r "\n"
+#define I_ADDDPP(r) "v_add_u32_dpp %" #r ", %" #r ", %" #r " wave_shr:1 row_mask:0xf bank_mask:0xf\n"
+#define I_MAXU(r) "v_max_u32_e32 %" #r ", %0, %" #r "\n"
+#define I_MED3(r) "v_med3_i32 %" #r ", %" #r ", %0, %1\n"
+#define I_LSHLOR(r) "v_lshl_or_b32 %" #r ", %" #r ", 1, %0\n"
+#define I_PERM(r) "v_perm_b32 %" #r ", %" #r ", %0, %1\n"
+#define I_ADDCO(r) "v_add_co_u32_e32 %" #r ", vcc, %0, %" #r "\n"
+#define I_MAXDPP8(r) "v_max_i32_dpp %" #r ", %" #r ", %" #r " row_shr:8 row_mask:0xf bank_mask:0xf\n"
 #define I_PAIR(r) "v_cmp_eq_i32_e32 vcc, %" #r ", %0\n v_addc_co_u32_e32 %1, vcc, %1, %1, vcc\n"
         if (MODE == 0) asm volatile(R32(I_ADD) OPS);
         if (MODE == 1) asm volatile(R32(I_MAX3) OPS);
@@ -69,6 +84,21 @@ __global__ void k(int* out, long long* cyc, int n) {
         if (MODE == 19) asm volatile(R32(I_DSW1) OPS);
         if (MODE == 20) asm volatile(R8(I_PAIR) R8(I_PAIR) OPS);
         if (MODE == 21) asm volatile("s_mov_b64 %8, 0x1234\n" R32(I_SST) OPS);
+        if (MODE == 22) asm volatile(R32(I_AND) OPS);
+        if (MODE == 23) asm volatile(R32(I_XOR) OPS);
+        if (MODE == 24) asm volatile(R32(I_LSR) OPS);
+        if (MODE == 25) asm volatile(R32(I_MOV) OPS);
+        if (MODE == 26) asm volatile(R32(I_ALIGN) OPS);
+        if (MODE == 27) asm volatile(R32(I_ADDSDWA) OPS);
+        if (MODE == 28) asm volatile(R32(I_CMPSDWA) OPS);
+        if (MODE == 29) asm volatile(R32(I_SUBREV) OPS);
+        if (MODE == 30) asm volatile(R32(I_ADDDPP) OPS);
+        if (MODE == 31) asm volatile(R32(I_MAXU) OPS);
+        if (MODE == 32) asm volatile(R32(I_MED3) OPS);
+        if (MODE == 33) asm volatile(R32(I_LSHLOR) OPS);
+        if (MODE == 34) asm volatile(R32(I_PERM) OPS);
+        if (MODE == 35) asm volatile(R32(I_ADDCO) OPS);
+        if (MODE == 36) asm volatile(R32(I_MAXDPP8) OPS);
     }
     if (MODE == 21) asm volatile("s_dcache_wb" ::: "memory");
     long long t1 = clock64();
@@ -86,12 +116,16 @@ int main() {
                            "v_cndmask_e64 (sgpr)", "v_add3_u32", "ds_write_b32", "global_store_dword",
                            "s_nop 1", "s_bfe_u64 (salu)", "v_cmp_e32 -> vcc", "v_addc_e32 (vcc)",
                            "v_cndmask_e32 (vcc)", "v_max_i32_e32", "v_sub_u32_e32", "ds_write_b32 stride1",
-                           "cmp_e32+addc_e32 pair/2", "s_store_dwordx2"};
-    void (*ks[])(int*, long long*, int) = {k<0>,  k<1>,  k<2>,  k<3>,  k<4>,  k<5>,  k<6>,
-                                           k<7>,  k<8>,  k<9>,  k<10>, k<11>, k<12>, k<13>,
-                                           k<14>, k<15>, k<16>, k<17>, k<18>, k<19>, k<20>, k<21>};
+                           "cmp_e32+addc_e32 pair/2", "s_store_dwordx2", "v_and_b32", "v_xor_b32",
+                           "v_lshrrev_b32", "v_mov_b32", "v_alignbit_b32", "v_add_u32_sdwa byte", "v_cmp_eq_sdwa byte",
+                           "v_subrev_u32", "v_add_u32_dpp wave_shr", "v_max_u32_e32", "v_med3_i32", "v_lshl_or_b32",
+                           "v_perm_b32", "v_add_co_u32_e32", "dpp max row_shr:8"};
+    void (*ks[])(int*, long long*, int) = {k<0>,  k<1>,  k<2>,  k<3>,  k<4>,  k<5>,  k<6>,  k<7>,  k<8>,  k<9>,
+                                           k<10>, k<11>, k<12>, k<13>, k<14>, k<15>, k<16>, k<17>, k<18>, k<19>,
+                                           k<20>, k<21>, k<22>, k<23>, k<24>, k<25>, k<26>, k<27>, k<28>, k<29>,
+                                           k<30>, k<31>, k<32>, k<33>, k<34>, k<35>, k<36>};
     printf("%-24s %s\n", "instruction", "clk/instr per wave @ 1,2,3,4 waves/SIMD  -> SIMD clk per instr");
-    for (int m = 0; m < 22; ++m) {
+    for (int m = 0; m < 37; ++m) {
         printf("%-24s", names[m]);
         double occ = 0;
         for (int wps = 1; wps <= 4; ++wps) {
