@@ -58,7 +58,8 @@ OUT = os.path.join(ROOT, "needleman-wunsch_amd", "csrc", "nw_chunk.inc")
 READ_STEP = 2          # first step whose gaps may issue the next slot's reads
 STORE = "normal"       # score stores: normal | fixed (diagnostic: one address)
 STORE_HINT = "nt"      # cache-policy bits of the score stores (e.g. "nt", "sc1")
-SCORE_X4 = False       # scores leave as 2 x global_store_dwordx4 per chunk from C++ (quad tiles)
+SCORE_X4 = True        # scores leave as 2 x global_store_dwordx4 per chunk from C++ (quad tiles)
+CODE_HINT = "nt"       # cache-policy bits of the code-word stores
 
 
 def gname(s):
@@ -94,25 +95,26 @@ class Item:
 def code_items(s, sh, SD):
     """Flags of column s-1 (sh = register holding wave_shr1 of G'_{s-1}) into its word.
 
-    Every candidate X is <= G'_{s-1} (it is a max over them), so X == G' exactly
-    when (G' - 1) - X < 0: the flag is the sign bit of one cheap VOP2
-    subtraction, shifted into the word by v_alignbit_b32 (acc << 1 | d >> 31).
+    Every candidate X is <= G'_{s-1} (G' is their max), so X - G' is 0 for a
+    candidate that attains the max and negative otherwise: the sign bit of one
+    cheap v_sub is the INVERTED flag, shifted into the word by v_alignbit_b32
+    (acc << 1 | d >> 31).  The word is inverted back once per chunk (MV).
     Neighbouring scores differ by a few |m|+|k|+|d|, so the subtraction cannot
     wrap.
     """
     Gp, Gpp, DGp = gname(s - 1), gname(s - 2), dg_reg(s - 1)
     hi = "0" if s == 1 else "%[accp]"      # first code of this chunk's word starts from 0
-    items = [Item("G1", f"v_add_u32_e32 %[gm1], -1, %[{Gp}]"),
-             Item("L", f"v_sub_u32_e32 %[dL], %[gm1], %[{Gpp}]", ["G1"]),
-             Item("D", f"v_sub_u32_e32 %[dD], %[gm1], %[{DGp}]", ["G1"]),
-             Item("U", f"v_sub_u32_e32 %[dU], %[gm1], %[{sh}]", ["G1"], True),
+    items = [Item("L", f"v_sub_u32_e32 %[dL], %[{Gpp}], %[{Gp}]"),
+             Item("D", f"v_sub_u32_e32 %[dD], %[{DGp}], %[{Gp}]"),
+             Item("U", f"v_sub_u32_e32 %[dU], %[{sh}], %[{Gp}]", [], True),
              Item("b1", f"v_alignbit_b32 %[accp], {hi}, %[dL], 31", ["L"]),
              Item("b2", "v_alignbit_b32 %[accp], %[accp], %[dU], 31", ["U", "b1"], True),
              Item("b3", "v_alignbit_b32 %[accp], %[accp], %[dD], 31", ["D", "b2"], True)]
     if s == 0:                # the previous chunk's word is complete: hand it out (and store it)
-        items.append(Item("MV", "v_mov_b32_e32 %[acc], %[accp]", ["b3"], True))
+        items.append(Item("MV", "v_xor_b32_e32 %[acc], 0xffffff, %[accp]", ["b3"], True))
         if SD:                # (chunk 0 stores its garbage word into the stripe's pad row)
-            items.append(Item("CS", "global_store_dword %[dv], %[acc], %[db]", ["MV"], True))
+            hint = f" {CODE_HINT}" if CODE_HINT else ""
+            items.append(Item("CS", f"global_store_dword %[dv], %[acc], %[db]{hint}", ["MV"], True))
             items.append(Item("CV", "v_add_u32_e32 %[dv], 0x100, %[dv]", ["CS"], True))
     return items
 
@@ -292,9 +294,10 @@ def flush(N, F, H, A, S):
     if F:
         sh = shreg(s)
         items = {it.name: it.text for it in code_items(s, sh, False)}
-        out += [f"v_mov_b32_e32 %[{sh}], %[t{s - 1}]", items["G1"], items["L"], items["D"],
+        out += [f"v_mov_b32_e32 %[{sh}], %[t{s - 1}]", items["L"], items["D"],
                 f"v_mov_b32_dpp %[{sh}], %[{gname(s - 1)}] wave_shr:1 row_mask:0xf bank_mask:0xf",
-                items["U"], items["b1"], items["b2"], items["b3"]]
+                items["U"], items["b1"], items["b2"], items["b3"],
+                f"v_xor_b32_e32 %[accp], {hex((1 << 3 * N) - 1)}, %[accp]"]     # (flags were collected inverted)
     if H:
         out += [it.text for it in score_items(s, A, S)]
     out.append("ds_write_b32 %[cb], %[cv] offset:16")
@@ -311,7 +314,7 @@ OPERANDS = r'''
       [h0] "=&v"(r.h[0]), [h1] "=&v"(r.h[1]), [h2] "=&v"(r.h[2]), [h3] "=&v"(r.h[3]),                      \
       [h4] "=&v"(r.h[4]), [h5] "=&v"(r.h[5]), [h6] "=&v"(r.h[6]), [h7] "=&v"(r.h[7]),                      \
       [accp] "+v"(r.accp), [acc] "=&v"(r.acc), [gav] "+v"(r.gav), [tmp] "=&v"(tmp_),                      \
-      [gm1] "=&v"(gm1_), [dL] "=&v"(dL_), [dU] "=&v"(dU_), [dD] "=&v"(dD_),                                \
+      [dL] "=&v"(dL_), [dU] "=&v"(dU_), [dD] "=&v"(dD_),                                \
       [cv] "+v"(r.cv), [hv] "+v"(r.hv), [dv] "+v"(r.dv),         \
       [nlo] "+v"(r.nlo)                                                                                    \
     : [t0] "v"(ts.a[0]), [t1] "v"(ts.a[1]), [t2] "v"(ts.a[2]), [t3] "v"(ts.a[3]),                          \
@@ -336,16 +339,18 @@ def tf(b):
 
 
 def main():
-    global OUT, READ_STEP, STORE, STORE_HINT, SCORE_X4
+    global OUT, READ_STEP, STORE, STORE_HINT, SCORE_X4, CODE_HINT
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=OUT)
     ap.add_argument("--read-step", type=int, default=READ_STEP)
     ap.add_argument("--store", choices=("normal", "fixed"), default=STORE)
     ap.add_argument("--store-hint", default=STORE_HINT)
     ap.add_argument("--x4", type=int, default=int(SCORE_X4))
+    ap.add_argument("--code-hint", default=CODE_HINT)
     args = ap.parse_args()
     OUT, READ_STEP, STORE, STORE_HINT = args.out, args.read_step, args.store, args.store_hint
     SCORE_X4 = bool(args.x4)
+    CODE_HINT = args.code_hint
     parts = ["// GENERATED by tools/gen_chunk_asm.py -- do not edit; see the generator for the schedule.\n",
              f"#define NW_SCORE_X4 {int(SCORE_X4)}\n#define NW_SCORE_HINT \"{(' ' + STORE_HINT) if STORE_HINT else ''}\"\n",
              OPERANDS, FLUSH_OPERANDS,
@@ -354,7 +359,7 @@ def main():
              "                                          RingSlot& ns, int ra, int rd);\n"
              "template <bool SH, bool SD, bool ST, int N>\n"
              "__device__ __forceinline__ void flush_asm(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts, int ra);\n"]
-    decl = "    int tmp_, gm1_, dL_, dU_, dD_, sh0_, sh1_, sh2_;\n"
+    decl = "    int tmp_, dL_, dU_, dD_, sh0_, sh1_, sh2_;\n"
     unpack = ""
     for SH in (0, 1):
         for SD in (0, 1):
