@@ -144,6 +144,7 @@ struct ChunkConst {
     int cb;             // LDS address of ctr[2w] (ring counters, see the kernel)
     int32_t* hb;        // score tile base (moves every super-chunk, with hv)
     uint32_t* db;       // code tile base (moves every super-chunk, with dv)
+    uint32_t pl, ph;    // profile (P blocks): byte a = sub' of symbol code a (int8), a = 0..3 / 4..7
 };
 
 #include "nw_chunk.inc"
@@ -170,25 +171,25 @@ __device__ __forceinline__ int g_of(const ChunkRegs& r, int s) {
 
 // The last chunk of a stripe (n = 1..8 columns): block + flush.  Returns H
 // of the stripe's last column (for the score-only last column).
-template <bool SH, bool SD, bool ST, int N>
+template <bool SH, bool SD, bool ST, bool P, int N>
 __device__ __forceinline__ int run_last(ChunkRegs& r, const ChunkConst& k, const RingSlot& t, int ra) {
     RingSlot n;
-    chunk_asm<SH, SD, ST, N, false>(r, k, t, n, ra, 0);
+    chunk_asm<SH, SD, ST, P, N, false>(r, k, t, n, ra, 0);
     flush_asm<SH, SD, ST, N>(r, k, t, ra);
     if constexpr ((SH && !NW_SCORE_X4) || ST) return r.h[N - 1];
     else return g_of(r, N - 1) + r.nlo + k.kd[N - 1];
 }
-template <bool SH, bool SD, bool ST>
+template <bool SH, bool SD, bool ST, bool P>
 __device__ __forceinline__ int run_last_n(int n, ChunkRegs& r, const ChunkConst& k, const RingSlot& t, int ra) {
     switch (n) {
-        case 1: return run_last<SH, SD, ST, 1>(r, k, t, ra);
-        case 2: return run_last<SH, SD, ST, 2>(r, k, t, ra);
-        case 3: return run_last<SH, SD, ST, 3>(r, k, t, ra);
-        case 4: return run_last<SH, SD, ST, 4>(r, k, t, ra);
-        case 5: return run_last<SH, SD, ST, 5>(r, k, t, ra);
-        case 6: return run_last<SH, SD, ST, 6>(r, k, t, ra);
-        case 7: return run_last<SH, SD, ST, 7>(r, k, t, ra);
-        default: return run_last<SH, SD, ST, 8>(r, k, t, ra);
+        case 1: return run_last<SH, SD, ST, P, 1>(r, k, t, ra);
+        case 2: return run_last<SH, SD, ST, P, 2>(r, k, t, ra);
+        case 3: return run_last<SH, SD, ST, P, 3>(r, k, t, ra);
+        case 4: return run_last<SH, SD, ST, P, 4>(r, k, t, ra);
+        case 5: return run_last<SH, SD, ST, P, 5>(r, k, t, ra);
+        case 6: return run_last<SH, SD, ST, P, 6>(r, k, t, ra);
+        case 7: return run_last<SH, SD, ST, P, 7>(r, k, t, ra);
+        default: return run_last<SH, SD, ST, P, 8>(r, k, t, ra);
     }
 }
 
@@ -222,11 +223,16 @@ __device__ __forceinline__ void store_chunk_scores(const ChunkRegs& r, const Chu
         qa = v4i{r.g[0] + nl + k.kd[0], r.g[1] + nl + k.kd[1], r.g[2] + nl + k.kd[2], r.g[3] + nl + k.kd[3]};
         qb = v4i{r.g[4] + nl + k.kd[4], r.g[5] + nl + k.kd[5], r.gp6 + nl + k.kd[6], r.gin + nl + k.kd[7]};
     }
+#ifdef NW_DIAG_FIXED_SCORES
+    const int hv = (int)(threadIdx.x & 63) * 16;   // diagnostic: no score traffic beyond one line per lane
+#else
+    const int hv = r.hv;
+#endif
     asm volatile(
         "global_store_dwordx4 %[hv], %[qa], %[hb]" NW_SCORE_HINT "\n\t"
         "global_store_dwordx4 %[hv], %[qb], %[hb] offset:1024" NW_SCORE_HINT
         :
-        : [hv] "v"(r.hv), [qa] "v"(qa), [qb] "v"(qb), [hb] "s"(k.hb)
+        : [hv] "v"(hv), [qa] "v"(qa), [qb] "v"(qb), [hb] "s"(k.hb)
         : "memory");
 }
 #endif
@@ -265,7 +271,7 @@ __device__ __forceinline__ void lds_publish(int* p, int v) {
 // hand-off loads are exact, and the compute waves never wait on vmcnt.
 // Granules (between workgroups and panels) carry H - d of the row above in
 // the plain domain; ring slots carry G'.
-template <int W, bool SH, bool SD, bool ST>
+template <int W, bool SH, bool SD, bool ST, bool PROF>
 __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
     constexpr int R = 4;
     constexpr bool F = SD || ST;     // direction codes
@@ -417,6 +423,18 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             asm volatile("" : "+v"(kc.cb));
             kc.hb = tile;
             kc.db = dtile;
+            // Profile (sequences coded 0..7 on the host): sub' of every
+            // symbol for this lane's side symbol, one int8 per code; a v_perm
+            // with the chunk's codes as selector looks up 4 columns at once.
+            kc.pl = kc.ph = 0;
+            if (PROF) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const uint32_t b = (uint32_t)((uint32_t)q == kc.c2 ? vcm : vck) & 0xffu;
+                    if (q < 4) kc.pl |= b << (8 * q);
+                    else kc.ph |= b << (8 * (q - 4));
+                }
+            }
             ChunkRegs r;
             // column 0: H[0][j] = -j*d (computation.c:112-120) -> G' = -(1 + row_base + 64*g0)*d
             r.gin = -(1 + a.row_base + 64 * g0) * d;
@@ -446,6 +464,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
                 a.trace[8 * (int64_t)sidx + 1] = __builtin_amdgcn_s_memrealtime();
                 a.trace[8 * (int64_t)sidx + 4] = __builtin_amdgcn_s_memtime();
             }
+            const bool trace_start = a.trace && lane == 0 && w == nw - 1;   // [6]: last wave's first block
             RingSlot tA, tB;
             // Slow path: wait until chunk c's ring slot is filled and our
             // consumer has room, re-reading the slot with every progress read.
@@ -516,7 +535,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
 #if NW_SCORE_X4
                 const int nl = r.nlo;
 #endif
-                chunk_asm<SH, SD, ST, 8, true>(r, kc, cur, nxt, ra[Q], rd[NQ]);
+                chunk_asm<SH, SD, ST, PROF, 8, true>(r, kc, cur, nxt, ra[Q], rd[NQ]);
 #if NW_SCORE_X4
                 if (SH) {
                     store_chunk_scores(r, kc, nl, ST);
@@ -535,6 +554,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             int c = 0;
             const int nfull = NC - 1;              // chunks before the last one
             bool aborted = !wait_slot(0, rd[0], tA);
+            if (trace_start) a.trace[8 * (int64_t)sidx + 6] = __builtin_amdgcn_s_memrealtime();
             while (c + R <= nfull && !aborted) {
                 rebase(c);
                 aborted = !full_chunk(c, S0{}, tA, tB) || !full_chunk(c + 1, S1{}, tB, tA) ||
@@ -556,7 +576,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
 #if NW_SCORE_X4
                 const int nl = r.nlo;
 #endif
-                const int hl = run_last_n<SH, SD, ST>(nlast, r, kc, tA, ring0 + slot * SLOT * 4);
+                const int hl = run_last_n<SH, SD, ST, PROF>(nlast, r, kc, tA, ring0 + slot * SLOT * 4);
 #if NW_SCORE_X4
                 // (columns past the last one land in the tile's own padding)
                 if (SH) store_chunk_scores(r, kc, nl, ST);
@@ -691,27 +711,32 @@ __global__ void nw_colhash_kernel(TableView v, int32_t L1, int32_t L2, uint64_t*
 // --------------------------------------------------------------- host side
 using KernelFn = void (*)(FillArgs);
 
-template <int W>
+template <int W, bool P>
 KernelFn pick_flags(bool sh, bool sd, bool stt) {
-    if (sh && sd) return stt ? nw_fill_kernel<W, true, true, true> : nw_fill_kernel<W, true, true, false>;
-    if (sh) return stt ? nw_fill_kernel<W, true, false, true> : nw_fill_kernel<W, true, false, false>;
-    if (sd) return stt ? nw_fill_kernel<W, false, true, true> : nw_fill_kernel<W, false, true, false>;
-    return stt ? nw_fill_kernel<W, false, false, true> : nw_fill_kernel<W, false, false, false>;
+    if (sh && sd) return stt ? nw_fill_kernel<W, true, true, true, P> : nw_fill_kernel<W, true, true, false, P>;
+    if (sh) return stt ? nw_fill_kernel<W, true, false, true, P> : nw_fill_kernel<W, true, false, false, P>;
+    if (sd) return stt ? nw_fill_kernel<W, false, true, true, P> : nw_fill_kernel<W, false, true, false, P>;
+    return stt ? nw_fill_kernel<W, false, false, true, P> : nw_fill_kernel<W, false, false, false, P>;
 }
 
-KernelFn pick_kernel(int W, bool sh, bool sd, bool stt) {
+template <int W>
+KernelFn pick_prof(bool prof, bool sh, bool sd, bool stt) {
+    return prof ? pick_flags<W, true>(sh, sd, stt) : pick_flags<W, false>(sh, sd, stt);
+}
+
+KernelFn pick_kernel(int W, bool prof, bool sh, bool sd, bool stt) {
     switch (W) {
-        case 1: return pick_flags<1>(sh, sd, stt);
-        case 2: return pick_flags<2>(sh, sd, stt);
-        case 3: return pick_flags<3>(sh, sd, stt);
-        case 4: return pick_flags<4>(sh, sd, stt);
-        case 5: return pick_flags<5>(sh, sd, stt);
-        case 6: return pick_flags<6>(sh, sd, stt);
-        case 7: return pick_flags<7>(sh, sd, stt);
-        case 8: return pick_flags<8>(sh, sd, stt);
-        case 10: return pick_flags<10>(sh, sd, stt);
-        case 12: return pick_flags<12>(sh, sd, stt);
-        case 15: return pick_flags<15>(sh, sd, stt);
+        case 1: return pick_prof<1>(prof, sh, sd, stt);
+        case 2: return pick_prof<2>(prof, sh, sd, stt);
+        case 3: return pick_prof<3>(prof, sh, sd, stt);
+        case 4: return pick_prof<4>(prof, sh, sd, stt);
+        case 5: return pick_prof<5>(prof, sh, sd, stt);
+        case 6: return pick_prof<6>(prof, sh, sd, stt);
+        case 7: return pick_prof<7>(prof, sh, sd, stt);
+        case 8: return pick_prof<8>(prof, sh, sd, stt);
+        case 10: return pick_prof<10>(prof, sh, sd, stt);
+        case 12: return pick_prof<12>(prof, sh, sd, stt);
+        case 15: return pick_prof<15>(prof, sh, sd, stt);
         default: return nullptr;
     }
 }
@@ -794,7 +819,13 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
     if (L1 > 0 && L2 > 0) {
         const StripePlan plan = plan_stripes(t->NG, t->ncu);
         W = plan.W;
-        KernelFn fn = pick_kernel(W, sh, sd, stt);
+        // Profile lookups when the sequences were coded to <= 8 symbols and
+        // sub' fits a signed byte ($NW_PROF=0 forces the byte compares).
+        const int64_t vcm = (int64_t)m + 2 * (int64_t)d, vck = 2 * (int64_t)d - k;
+        const char* pe = getenv("NW_PROF");
+        const bool prof = t->alpha > 0 && vcm >= -128 && vcm <= 127 && vck >= -128 && vck <= 127 &&
+                          !(pe && atoi(pe) == 0);
+        KernelFn fn = pick_kernel(W, prof, sh, sd, stt);
         if (!fn) return fail(NW_ERR_ARG, "nw_table_fill: unsupported wave count");
         FillArgs a{};
         a.s1 = t->s1;
@@ -1030,8 +1061,34 @@ int nw_table_set_sequences(nw_table* t, const char* s1, int64_t L1, const char* 
     const size_t n1 = (size_t)(CH * t->NC + 64), n2 = (size_t)(64 * t->NG + 1024);
     HIPCHK(hipMemsetAsync(t->s1, 0, n1, t->stream));
     HIPCHK(hipMemsetAsync(t->s2, 0, n2, t->stream));
-    if (L1) HIPCHK(hipMemcpyAsync(t->s1, s1, (size_t)L1, hipMemcpyHostToDevice, t->stream));
-    if (L2) HIPCHK(hipMemcpyAsync(t->s2, s2, (size_t)L2, hipMemcpyHostToDevice, t->stream));
+    // Only equality of symbols matters (needleman-wunsch.c:432), so when
+    // s1 and s2 use at most 8 distinct bytes they are coded 0..7 (in order of
+    // first appearance) and the fill looks sub' up in a per-lane profile.
+    int code[256];
+    std::fill(code, code + 256, -1);
+    int alpha = 0;
+    auto scan = [&](const char* p, int64_t n) {
+        for (int64_t i = 0; i < n && alpha <= 8; ++i) {
+            const uint8_t b = (uint8_t)p[i];
+            if (code[b] < 0) code[b] = alpha++;
+        }
+    };
+    scan(s1, L1);
+    scan(s2, L2);
+    t->alpha = (alpha >= 1 && alpha <= 8) ? alpha : 0;
+    std::vector<uint8_t> c1, c2;
+    const void* src1 = s1;
+    const void* src2 = s2;
+    if (t->alpha) {
+        c1.resize((size_t)L1);
+        c2.resize((size_t)L2);
+        for (int64_t i = 0; i < L1; ++i) c1[(size_t)i] = (uint8_t)code[(uint8_t)s1[i]];
+        for (int64_t i = 0; i < L2; ++i) c2[(size_t)i] = (uint8_t)code[(uint8_t)s2[i]];
+        src1 = c1.data();
+        src2 = c2.data();
+    }
+    if (L1) HIPCHK(hipMemcpyAsync(t->s1, src1, (size_t)L1, hipMemcpyHostToDevice, t->stream));
+    if (L2) HIPCHK(hipMemcpyAsync(t->s2, src2, (size_t)L2, hipMemcpyHostToDevice, t->stream));
     HIPCHK(hipStreamSynchronize(t->stream));
     return NW_OK;
 }

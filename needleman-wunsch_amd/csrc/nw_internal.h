@@ -18,6 +18,7 @@ struct nw_table {
     // geometry for the current sequences
     int64_t L1 = -1, L2 = -1;
     int64_t NC = 0, NG = 0, spitch = 0;
+    int alpha = 0;                  // s1/s2 coded to symbols 0..alpha-1 on the device (<= 8), 0: raw bytes
     // device buffers
     uint8_t* s1 = nullptr;
     uint8_t* s2 = nullptr;

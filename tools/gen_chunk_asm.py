@@ -151,7 +151,7 @@ def sub_items(b):
             Item("X", f"v_cndmask_b32_e64 %[{sub_reg(b)}], %[vck], %[vcm], vcc", ["M"])]
 
 
-def floating_items(N, nxt):
+def floating_items(N, nxt, P=False):
     """Memory items with a window of steps [lo, hi]; issued in list order.
 
     Ring counters: cb = &ctr[2w], ctr[2v+2] = prog[v] (chunks in wave v's ring),
@@ -162,6 +162,8 @@ def floating_items(N, nxt):
     last = N - 1
     its = [Item(f"SH{s}", f"v_mov_b32_e32 %[{shreg(s)}], %[t{s - 1}]", lo=max(s - 2, 0), hi=s - 1)
            for s in range(1, N)]
+    if P and N > 4:                  # profile lookup of steps 4..7, before step 4
+        its.append(Item("PB", "v_perm_b32 %[subB], %[ph], %[pl], %[t9]", hi=3))
     its += [Item("CW", "ds_write_b32 %[cb], %[cv] offset:4", lds=True, hi=last),  # ring slot taken
            Item("W8", "ds_write_b32 %[ra], %[t8] offset:32", lds=True, hi=last),  # top-string bytes
            Item("W9", "ds_write_b32 %[ra], %[t9] offset:36", lds=True, hi=last)]  # go down the ring
@@ -179,23 +181,31 @@ def floating_items(N, nxt):
     return its
 
 
-def step(s, N, F, H, A, S, SD, nxt, floating):
+def step(s, N, F, H, A, S, SD, nxt, floating, P=False):
     Gp = gname(s - 1)
     Tm = shreg(s)
     fill = []
     if s == 0:
-        fill += sub_items(0)            # first gap: sub' of this step itself
+        if P:                           # first gap: sub' bytes of steps 0..3 (profile lookup)
+            fill.append(Item("PA", "v_perm_b32 %[subA], %[ph], %[pl], %[t8]"))
+        else:
+            fill += sub_items(0)        # first gap: sub' of this step itself
     if F:
         fill += code_items(s, Tm, SD)
     if s > 0:
         fill.append(ring_item(s))
     if H and s > 0:
         fill += score_items(s, A, S)
-    if s + 1 < N:
+    if s + 1 < N and not P:
         fill += sub_items(s + 1)
+    if P:                               # diagonal: sign-extended sub' byte of this step
+        add = (f"v_add_u32_sdwa %[{dg_reg(s)}], %[{Tm}], sext(%[{'subA' if s < 4 else 'subB'}]) "
+               f"dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_{s % 4}")
+    else:
+        add = f"v_add_u32_e32 %[{dg_reg(s)}], %[{Tm}], %[{sub_reg(s)}]"
     chain_head = [
         f"v_mov_b32_dpp %[{Tm}], %[{Gp}] wave_shr:1 row_mask:0xf bank_mask:0xf",
-        f"v_add_u32_e32 %[{dg_reg(s)}], %[{Tm}], %[{sub_reg(s)}]",
+        add,
         f"v_max3_i32 %[{gname(s)}], %[{Gp}], %[{dg_reg(s)}], %[t{s}]",
     ]
     dpps = ["row_shr:1 row_mask:0xf", "row_shr:2 row_mask:0xf", "row_shr:4 row_mask:0xf",
@@ -265,13 +275,13 @@ def resolve_waits(items):
     return text
 
 
-def block(N, F, H, A, S, SD, nxt):
+def block(N, F, H, A, S, SD, nxt, P=False):
     items = []
     if STORE == "fixed" and S and not SCORE_X4:     # diagnostic: every store to this lane's first word (hv = lane*4)
         items.append(Item("HF", "v_and_b32_e32 %[hv], 0xff, %[hv]"))
-    floating = floating_items(N, nxt)
+    floating = floating_items(N, nxt, P)
     for s in range(N):
-        items += step(s, N, F, H, A, S, SD, nxt, floating)
+        items += step(s, N, F, H, A, S, SD, nxt, floating, P)
     assert not floating, [f.name for f in floating]
     if nxt:                        # the chunk's last column (G'_7 is final now)
         items.append(ring_item(8))
@@ -322,7 +332,8 @@ OPERANDS = r'''
       [t9] "v"(ts.c[1]), [c2] "v"(k.c2), [vcm] "v"(k.vcm), [vck] "v"(k.vck), [d8] "s"(k.d8),                                \
       [k0] "v"(k.kd[0]), [k1] "v"(k.kd[1]), [k2] "v"(k.kd[2]), [k3] "v"(k.kd[3]),                          \
       [k4] "v"(k.kd[4]), [k5] "v"(k.kd[5]), [k6] "v"(k.kd[6]), [k7] "v"(k.kd[7]),                          \
-      [ra] "v"(ra), [rd] "v"(rd), [cb] "v"(k.cb), [hb] "s"(k.hb), [db] "s"(k.db)
+      [ra] "v"(ra), [rd] "v"(rd), [cb] "v"(k.cb), [hb] "s"(k.hb), [db] "s"(k.db), [pl] "v"(k.pl),         \
+      [ph] "v"(k.ph)
 '''
 # The flush reads values the chunk block produced: every value operand is read-write.
 FLUSH_OPERANDS = (OPERANDS.replace("NW_CHUNK_OPERANDS", "NW_FLUSH_OPERANDS")
@@ -354,7 +365,7 @@ def main():
     parts = ["// GENERATED by tools/gen_chunk_asm.py -- do not edit; see the generator for the schedule.\n",
              f"#define NW_SCORE_X4 {int(SCORE_X4)}\n#define NW_SCORE_HINT \"{(' ' + STORE_HINT) if STORE_HINT else ''}\"\n",
              OPERANDS, FLUSH_OPERANDS,
-             "template <bool SH, bool SD, bool ST, int N, bool NEXT>\n"
+             "template <bool SH, bool SD, bool ST, bool P, int N, bool NEXT>\n"
              "__device__ __forceinline__ void chunk_asm(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts,\n"
              "                                          RingSlot& ns, int ra, int rd);\n"
              "template <bool SH, bool SD, bool ST, int N>\n"
@@ -368,11 +379,12 @@ def main():
                 head = f"{tf(SH)}, {tf(SD)}, {tf(ST)}"
                 for N in range(1, 9):
                     for nxt in ((0, 1) if N == 8 else (0,)):
-                        parts.append(
-                            f"template <> __device__ __forceinline__ void chunk_asm<{head}, {N}, {tf(nxt)}>"
-                            f"(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts, RingSlot& ns, int ra, int rd) {{\n"
-                            f"{decl}{unpack}    asm volatile(\n{cstr(block(N, F, H, A, S, SD, nxt))}\n"
-                            f"        NW_CHUNK_OPERANDS : \"vcc\", \"scc\", \"memory\");\n}}\n")
+                        for P in (0, 1):
+                            parts.append(
+                                f"template <> __device__ __forceinline__ void chunk_asm<{head}, {tf(P)}, {N}, {tf(nxt)}>"
+                                f"(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts, RingSlot& ns, int ra, int rd) {{\n"
+                                f"{decl}{unpack}    asm volatile(\n{cstr(block(N, F, H, A, S, SD, nxt, P))}\n"
+                                f"        NW_CHUNK_OPERANDS : \"vcc\", \"scc\", \"memory\");\n}}\n")
                     parts.append(
                         f"template <> __device__ __forceinline__ void flush_asm<{head}, {N}>"
                         f"(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts, int ra) {{\n{decl}"

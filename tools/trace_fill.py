@@ -25,5 +25,12 @@ print(f"shader clock over stripe i (MHz): " + " ".join(f"{mhz[i]:.0f}" for i in 
 lag = np.diff(st) if n > 1 else np.zeros(1)
 print(f"start lag per stripe: mean {lag.mean():.2f} us  median {np.median(lag):.2f}  p90 {np.percentile(lag, 90):.2f}  max {lag.max():.2f}")
 print(f"stripe duration: first {dur[0]:.1f} us  median {np.median(dur):.1f}  last {dur[-1]:.1f}  max {dur.max():.1f}")
+lastw = (tr[:, 6] - t0) / 100.0
+nwv = max(t.waves - 1, 1)
+intra = (lastw - st) / nwv
+print(f"intra-WG lag per stripe (first -> last wave start)/(W-1): median {np.median(intra):.3f} us  p90 {np.percentile(intra, 90):.3f}")
+if n > 1:
+    hand = st[1:] - lastw[:-1]
+    print(f"WG-stripe hand-off (last wave start -> next WG first wave start): median {np.median(hand):.3f} us  p90 {np.percentile(hand, 90):.3f}  max {hand.max():.3f}")
 cu = (tr[:, 3] >> 32) & 0xffffffff
 print(f"distinct CU ids used: {len(set(cu.tolist()))}")
