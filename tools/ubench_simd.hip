@@ -45,7 +45,7 @@ __global__ void k(int* out, long long* cyc, int n) {
 #define I_MAX32(r) "v_max_i32_e32 %" #r ", %" #r ", %0\n"
 #define I_SUB32(r) "v_sub_u32_e32 %" #r ", %" #r ", %0\n"
 #define I_DSW1(r) "ds_write_b32 %15, %" #r " offset:" #r "*4\n"
-#define I_SST(r) "s_store_dwordx2 %8, %14, " #r "*8\n"
+#define I_OR(r) "v_or_b32_e32 %" #r ", %0, %" #r "\n"
 #define I_AND(r) "v_and_b32_e32 %" #r ", %0, %" #r "\n"
 #define I_XOR(r) "v_xor_b32_e32 %" #r ", %0, %" #r "\n"
 #define I_LSR(r) "v_lshrrev_b32_e32 %" #r ", 3, %" #r "\n"
@@ -83,7 +83,7 @@ __global__ void k(int* out, long long* cyc, int n) {
         if (MODE == 18) asm volatile(R32(I_SUB32) OPS);
         if (MODE == 19) asm volatile(R32(I_DSW1) OPS);
         if (MODE == 20) asm volatile(R8(I_PAIR) R8(I_PAIR) OPS);
-        if (MODE == 21) asm volatile("s_mov_b64 %8, 0x1234\n" R32(I_SST) OPS);
+        if (MODE == 21) asm volatile(R32(I_OR) OPS);
         if (MODE == 22) asm volatile(R32(I_AND) OPS);
         if (MODE == 23) asm volatile(R32(I_XOR) OPS);
         if (MODE == 24) asm volatile(R32(I_LSR) OPS);
@@ -100,7 +100,6 @@ __global__ void k(int* out, long long* cyc, int n) {
         if (MODE == 35) asm volatile(R32(I_ADDCO) OPS);
         if (MODE == 36) asm volatile(R32(I_MAXDPP8) OPS);
     }
-    if (MODE == 21) asm volatile("s_dcache_wb" ::: "memory");
     long long t1 = clock64();
     out[blockIdx.x * blockDim.x + threadIdx.x + 1000000] = v0 + v1 + v2 + v3 + v4 + v5 + v6 + v7 + (int)s0;
     if ((threadIdx.x & 63) == 0) cyc[threadIdx.x >> 6] = t1 - t0;
@@ -116,7 +115,7 @@ int main() {
                            "v_cndmask_e64 (sgpr)", "v_add3_u32", "ds_write_b32", "global_store_dword",
                            "s_nop 1", "s_bfe_u64 (salu)", "v_cmp_e32 -> vcc", "v_addc_e32 (vcc)",
                            "v_cndmask_e32 (vcc)", "v_max_i32_e32", "v_sub_u32_e32", "ds_write_b32 stride1",
-                           "cmp_e32+addc_e32 pair/2", "s_store_dwordx2", "v_and_b32", "v_xor_b32",
+                           "cmp_e32+addc_e32 pair/2", "v_or_b32", "v_and_b32", "v_xor_b32",
                            "v_lshrrev_b32", "v_mov_b32", "v_alignbit_b32", "v_add_u32_sdwa byte", "v_cmp_eq_sdwa byte",
                            "v_subrev_u32", "v_add_u32_dpp wave_shr", "v_max_u32_e32", "v_med3_i32", "v_lshl_or_b32",
                            "v_perm_b32", "v_add_co_u32_e32", "dpp max row_shr:8"};
