@@ -148,6 +148,30 @@ int64_t nw_table_trace(nw_table *t, uint64_t *dst, int64_t n);
 /* Waves per workgroup chosen for the last fill (tuning / reporting). */
 int nw_table_waves(const nw_table *t);
 
+/* ---------------------------------------------------------------------------
+ * Walk services: results of the reference's traceback that do not need its
+ * exponential enumeration, computed on the device from the direction codes of
+ * the last fill (which must have had NW_OUT_DIRS; whole tables only, not row
+ * panels).
+ *
+ * nw_table_count_alignments: the number of optimal alignments -- what the
+ * reference's walk counts (construct_alignments, needleman-wunsch.c:356-388;
+ * inc_solution_count at :250-255) and print_summary reports
+ * (computation.c:271-281) -- as the reference's `unsigned` counter, i.e.
+ * modulo 2^32.
+ */
+int nw_table_count_alignments(nw_table *t, uint32_t *count);
+
+/* nw_table_first_path: the first alignment the reference prints -- its walk
+ * tries diag, then left, then up (needleman-wunsch.c:296-322), so the first
+ * arrival at (0,0) is that greedy path from the corner.  moves[0..*n) gets
+ * the path in forward order ((0,0) to (L1,L2)): 1 = diag (s1[i] over s2[j]),
+ * 2 = up (gap over s2[j]), 4 = left (s1[i] over a gap).  cap >= L1 + L2. */
+int nw_table_first_path(nw_table *t, uint8_t *moves, int64_t cap, int64_t *n);
+
+/* Device time (ms) of the last count / first-path kernel (HIP events). */
+int nw_table_walk_elapsed_ms(nw_table *t, float *count_ms, float *path_ms);
+
 #ifdef __cplusplus
 }
 #endif

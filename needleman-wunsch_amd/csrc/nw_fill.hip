@@ -972,6 +972,7 @@ void nw_table_destroy(nw_table* t) {
     if (!t) return;
     (void)hipSetDevice(t->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);
+    nwi::walk_release(t);
     (void)hipFree(t->s1);
     (void)hipFree(t->s2);
     (void)hipFree(t->H);

@@ -8,6 +8,8 @@
 
 #include "nw_fill.h"
 
+struct nw_walk_state;   // nw_walk.hip: count / first-path buffers
+
 struct nw_table {
     int device = 0;
     int ncu = 256;
@@ -50,6 +52,7 @@ struct nw_table {
     nw_stats stats{};
     float kernel_ms = 0.f, call_ms = 0.f;
     int waves = 0;
+    nw_walk_state* walk = nullptr;  // lazily created by the walk services
 };
 
 namespace nwi {
@@ -65,6 +68,9 @@ int fill_finish(nw_table* t);
 // Write "producer failed" granules for `epoch` over p[0, n) (any device memory,
 // including a peer's mapped boundary buffer), on stream s.
 int poison(uint64_t* p, int64_t n, uint32_t epoch, hipStream_t s);
+
+// Free the walk services' buffers (nw_walk.hip); called by nw_table_destroy.
+void walk_release(nw_table* t);
 
 constexpr int kChunk = 8;   // columns per chunk (hand-off granules per chunk)
 

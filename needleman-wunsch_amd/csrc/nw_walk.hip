@@ -1,0 +1,326 @@
+// nw_walk.hip -- walk services over a device-resident filled table.
+//
+// The reference walks its table on the host after the fill
+// (construct_alignments, needleman-wunsch.c:356-388, iterating in
+// construct_alignments_for_subtable, :209-331): a depth-first enumeration of
+// every optimal alignment that prints each one and counts them
+// (inc_solution_count, :250-255; print_summary, computation.c:271-281).  The
+// enumeration is exponential, so at 100k x 100k the reference cannot even
+// report `-s`.  Two of its results do not need the enumeration and run here on
+// the device, straight from the direction codes the fill left in HBM:
+//
+//   * nw_table_count_alignments -- the number of optimal alignments is the
+//     number of code paths from the corner to (0,0): a path-count DP
+//     P(i,j) = [diag] P(i-1,j-1) + [left] P(i-1,j) + [up] P(i,j-1), P(0,0) = 1,
+//     in uint32 (the reference's counter is an `unsigned` that wraps the
+//     same way, walk-table.c:108-147).  Same stripe orientation as the fill:
+//     a wave owns 64 rows and sweeps the columns; the up term is an affine
+//     scan over the lanes (six DPP levels, like the fill's prefix max); the
+//     stripe below takes the bottom row through tagged granules.
+//   * nw_table_first_path -- the first alignment the reference prints is the
+//     greedy walk diag > left > up from the corner (:296-322).  One wave
+//     stages 64 rows x 64 columns of codes in LDS and walks them, O(L1 + L2).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "nw_internal.h"
+
+struct nw_walk_state {
+    uint64_t* rows = nullptr;     // count hand-off granules {tag, P}, (NG-1) x L1
+    size_t rows_bytes = 0;
+    uint32_t epoch = 0;           // tag of the count in flight
+    uint32_t* ctl = nullptr;      // [0] dequeue, [1] abort, [2] result, [3] path length lo, [4] hi / error
+    uint8_t* moves = nullptr;     // first path, back to front
+    size_t moves_bytes = 0;
+    float count_ms = 0.f, path_ms = 0.f;
+};
+
+namespace {
+
+constexpr int CBLK = 16;                       // columns per count hand-off block
+constexpr int64_t WALK_SPIN = 1000000000;      // 10 s of s_memrealtime (100 MHz)
+constexpr uint32_t POISON = 0x80000000u;
+
+struct CountArgs {
+    const uint32_t* D;    // codes, include/nw_fill.h layout
+    int64_t NC;           // 8-column chunks of the current L1
+    int32_t L1, L2, NG;
+    uint64_t* rows;       // granule (g, i) at g*L1 + i-1: P(i, 64(g+1)) for stripe g < NG-1
+    uint32_t* ctl;
+    uint32_t epoch;
+};
+
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void scan_level(uint32_t& A, uint32_t& u) {
+    const uint32_t Ap = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)A, CTRL, ROWMASK, 0xf, false);
+    const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)u, CTRL, ROWMASK, 0xf, false);
+    A += Ap & u;
+    u &= up;
+}
+
+// One wave per 64-row stripe, stripes taken in order from a ticket counter,
+// so a wave only ever waits for a stripe already held by a running wave.
+__global__ __launch_bounds__(64) void nw_count_kernel(CountArgs a) {
+    const int lane = threadIdx.x;
+    const uint32_t tag = a.epoch;
+    for (;;) {
+        int g = 0;
+        if (lane == 0) g = (int)atomicAdd(&a.ctl[0], 1u);
+        g = __builtin_amdgcn_readfirstlane(g);
+        if (g >= a.NG) return;
+        if (__hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+
+        const uint32_t* Dg = a.D + ((int64_t)g * (a.NC + 1) + 1) * 64 + lane;
+        const uint64_t* top = g > 0 ? a.rows + (int64_t)(g - 1) * a.L1 : nullptr;
+        uint64_t* bot = g < a.NG - 1 ? a.rows + (int64_t)g * a.L1 : nullptr;
+        uint32_t P = 1;         // column 0: (0,j) has only the up code, P = 1
+        uint32_t Tprev = 1;     // P(0, 64g)
+        uint32_t w = 0, wn = a.NC > 0 ? Dg[0] : 0u;
+        bool dead = false;
+        for (int i0 = 1; i0 <= a.L1 && !dead; i0 += CBLK) {
+            const int cnt = min(CBLK, a.L1 - i0 + 1);
+            uint32_t Tv = 1;    // stripe 0: P(i, 0) = 1 (left codes)
+            if (top) {
+                uint64_t gv = 0;
+                const int64_t t0 = __builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    if (lane < cnt)
+                        gv = __hip_atomic_load(top + i0 - 1 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t gt = (uint32_t)(gv >> 32);
+                    const bool ok = lane >= cnt || gt == tag;
+                    const bool bad = lane < cnt && gt == (tag | POISON);
+                    if (__builtin_amdgcn_ballot_w64(bad)) {
+                        dead = true;
+                        break;
+                    }
+                    if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > WALK_SPIN) {
+                        if (lane == 0) __hip_atomic_store(&a.ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        dead = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (dead) break;
+                Tv = (uint32_t)gv;
+            }
+            uint32_t outv = 0;
+            for (int c = 0; c < cnt; ++c) {
+                const int i = i0 + c;
+                const int s = (i - 1) & 7;
+                if (s == 0) {
+                    w = wn;
+                    const int64_t qn = ((i - 1) >> 3) + 1;
+                    if (qn < a.NC) wn = Dg[qn * 64];
+                }
+                const uint32_t code = (w >> (21 - 3 * s)) & 7u;
+                const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)Tv, c);
+                const uint32_t diag = (uint32_t)__builtin_amdgcn_update_dpp((int)Tprev, (int)P, 0x138, 0xf, 0xf, false);
+                uint32_t A = ((code & 1u) ? diag : 0u) + ((code & 4u) ? P : 0u);
+                uint32_t u = (code & 2u) ? ~0u : 0u;
+                scan_level<0x111, 0xf>(A, u);
+                scan_level<0x112, 0xf>(A, u);
+                scan_level<0x114, 0xf>(A, u);
+                scan_level<0x118, 0xf>(A, u);
+                scan_level<0x142, 0xa>(A, u);
+                scan_level<0x143, 0xc>(A, u);
+                P = A + (u & T);
+                Tprev = T;
+                const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)P, 63);
+                if (lane == c) outv = b;
+            }
+            if (bot && lane < cnt)
+                __hip_atomic_store(bot + i0 - 1 + lane, ((uint64_t)tag << 32) | outv, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (dead) {
+            // Tell the stripe below (and everything after it) to stop.
+            if (bot)
+                for (int x = lane; x < a.L1; x += 64)
+                    __hip_atomic_store(bot + x, (uint64_t)(tag | POISON) << 32, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        if (g == (a.L2 - 1) / 64 && lane == (a.L2 - 1) % 64) a.ctl[2] = P;
+    }
+}
+
+// Greedy walk diag > left > up from (L1, L2) to (0, 0).  Moves are written
+// back to front; ctl[3] = count, ctl[4] = 1 if a cell had no code.
+__global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, int64_t NC, int32_t L1, int32_t L2,
+                                                           uint8_t* moves, uint32_t* ctl) {
+    __shared__ uint32_t blk[8][64];
+    const int lane = threadIdx.x;
+    int i = L1, j = L2;
+    uint32_t n = 0;
+    int gb = -1;
+    int64_t qb = -1;
+    while (i > 0 && j > 0) {
+        const int g = (j - 1) >> 6;
+        const int64_t q = (i - 1) >> 3, q0 = q & ~(int64_t)7;
+        if (g != gb || q0 != qb) {
+            __syncthreads();
+#pragma unroll
+            for (int x = 0; x < 8; ++x)
+                blk[x][lane] = q0 + x < NC ? D[((int64_t)g * (NC + 1) + q0 + x + 1) * 64 + lane] : 0u;
+            __syncthreads();
+            gb = g;
+            qb = q0;
+        }
+        const uint32_t code = (blk[q - q0][(j - 1) & 63] >> (21 - 3 * ((i - 1) & 7))) & 7u;
+        uint8_t mv;
+        if (code & 1u) {
+            mv = 1;
+            --i;
+            --j;
+        } else if (code & 4u) {
+            mv = 4;
+            --i;
+        } else if (code & 2u) {
+            mv = 2;
+            --j;
+        } else {
+            if (lane == 0) ctl[4] = 1;
+            return;
+        }
+        if (lane == 0) moves[n] = mv;
+        ++n;
+    }
+    for (; j > 0; --j, ++n)      // column 0: up codes
+        if (lane == 0) moves[n] = 2;
+    for (; i > 0; --i, ++n)      // row 0: left codes
+        if (lane == 0) moves[n] = 4;
+    if (lane == 0) ctl[3] = n;
+}
+
+int check_walkable(nw_table* t, const char* who) {
+    if (!t) return nwi::fail(NW_ERR_ARG, std::string(who) + ": NULL table");
+    if (!t->filled || !(t->last_mask & NW_OUT_DIRS))
+        return nwi::fail(NW_ERR_STATE, std::string(who) + ": no direction codes (fill with NW_OUT_DIRS first)");
+    if (t->row_base > 0 || t->xout)
+        return nwi::fail(NW_ERR_STATE, std::string(who) + ": a row panel is not a whole table");
+    return NW_OK;
+}
+
+int walk_state(nw_table* t, nw_walk_state** out) {
+    if (!t->walk) {
+        t->walk = new nw_walk_state;
+        NW_HIPCHK(hipMalloc(&t->walk->ctl, 64));
+    }
+    *out = t->walk;
+    return NW_OK;
+}
+
+}  // namespace
+
+namespace nwi {
+
+void walk_release(nw_table* t) {
+    if (!t || !t->walk) return;
+    (void)hipFree(t->walk->rows);
+    (void)hipFree(t->walk->ctl);
+    (void)hipFree(t->walk->moves);
+    delete t->walk;
+    t->walk = nullptr;
+}
+
+}  // namespace nwi
+
+extern "C" {
+
+int nw_table_count_alignments(nw_table* t, uint32_t* count) {
+    int rc = check_walkable(t, "nw_table_count_alignments");
+    if (rc) return rc;
+    if (!count) return nwi::fail(NW_ERR_ARG, "nw_table_count_alignments: NULL count");
+    if (t->L1 == 0 || t->L2 == 0) {   // one path along the seeded row or column
+        *count = 1;
+        return NW_OK;
+    }
+    NW_HIPCHK(hipSetDevice(t->device));
+    nw_walk_state* w = nullptr;
+    if ((rc = walk_state(t, &w))) return rc;
+    const int64_t NG = t->NG;
+    const size_t need = (size_t)std::max<int64_t>(NG - 1, 1) * (size_t)t->L1 * 8;
+    if (need > w->rows_bytes) {
+        (void)hipFree(w->rows);
+        w->rows = nullptr;
+        w->rows_bytes = 0;
+        NW_HIPCHK(hipMalloc(&w->rows, need));
+        NW_HIPCHK(hipMemsetAsync(w->rows, 0, need, t->stream));
+        w->rows_bytes = need;
+    }
+    if (++w->epoch & POISON) w->epoch = 1;   // tags stay below the poison bit
+    CountArgs a{};
+    a.D = t->D;
+    a.NC = t->NC;
+    a.L1 = (int32_t)t->L1;
+    a.L2 = (int32_t)t->L2;
+    a.NG = (int32_t)NG;
+    a.rows = w->rows;
+    a.ctl = w->ctl;
+    a.epoch = w->epoch;
+    NW_HIPCHK(hipMemsetAsync(w->ctl, 0, 64, t->stream));
+    const int grid = (int)std::min<int64_t>(NG, 8 * (int64_t)t->ncu);
+    NW_HIPCHK(hipEventRecord(t->ev[2], t->stream));
+    nw_count_kernel<<<grid, 64, 0, t->stream>>>(a);
+    NW_HIPCHK(hipGetLastError());
+    NW_HIPCHK(hipEventRecord(t->ev[3], t->stream));
+    uint32_t ctl[8];
+    NW_HIPCHK(hipMemcpyAsync(ctl, w->ctl, sizeof ctl, hipMemcpyDeviceToHost, t->stream));
+    NW_HIPCHK(hipStreamSynchronize(t->stream));
+    (void)hipEventElapsedTime(&w->count_ms, t->ev[2], t->ev[3]);
+    if (ctl[1]) return nwi::fail(NW_ERR_TIMEOUT, "nw_table_count_alignments: stripe hand-off watchdog fired");
+    *count = ctl[2];
+    return NW_OK;
+}
+
+int nw_table_first_path(nw_table* t, uint8_t* moves, int64_t cap, int64_t* n) {
+    int rc = check_walkable(t, "nw_table_first_path");
+    if (rc) return rc;
+    if (!n || (cap > 0 && !moves) || cap < 0) return nwi::fail(NW_ERR_ARG, "nw_table_first_path: bad arguments");
+    const int64_t most = t->L1 + t->L2;
+    if (cap < most) return nwi::fail(NW_ERR_ARG, "nw_table_first_path: cap < L1 + L2");
+    NW_HIPCHK(hipSetDevice(t->device));
+    nw_walk_state* w = nullptr;
+    if ((rc = walk_state(t, &w))) return rc;
+    if ((size_t)std::max<int64_t>(most, 1) > w->moves_bytes) {
+        (void)hipFree(w->moves);
+        w->moves = nullptr;
+        w->moves_bytes = 0;
+        NW_HIPCHK(hipMalloc(&w->moves, (size_t)std::max<int64_t>(most, 1)));
+        w->moves_bytes = (size_t)std::max<int64_t>(most, 1);
+    }
+    NW_HIPCHK(hipMemsetAsync(w->ctl, 0, 64, t->stream));
+    NW_HIPCHK(hipEventRecord(t->ev[2], t->stream));
+    nw_first_path_kernel<<<1, 64, 0, t->stream>>>(t->D, t->NC, (int32_t)t->L1, (int32_t)t->L2, w->moves, w->ctl);
+    NW_HIPCHK(hipGetLastError());
+    NW_HIPCHK(hipEventRecord(t->ev[3], t->stream));
+    uint32_t ctl[8];
+    NW_HIPCHK(hipMemcpyAsync(ctl, w->ctl, sizeof ctl, hipMemcpyDeviceToHost, t->stream));
+    NW_HIPCHK(hipStreamSynchronize(t->stream));
+    (void)hipEventElapsedTime(&w->path_ms, t->ev[2], t->ev[3]);
+    if (ctl[4]) return nwi::fail(NW_ERR_STATE, "nw_table_first_path: a cell on the path has no direction code");
+    const int64_t len = ctl[3];
+    if (len > most) return nwi::fail(NW_ERR_HIP, "nw_table_first_path: path longer than L1 + L2");
+    if (len > 0) {
+        NW_HIPCHK(hipMemcpyAsync(moves, w->moves, (size_t)len, hipMemcpyDeviceToHost, t->stream));
+        NW_HIPCHK(hipStreamSynchronize(t->stream));
+    }
+    std::reverse(moves, moves + len);
+    *n = len;
+    return NW_OK;
+}
+
+int nw_table_walk_elapsed_ms(nw_table* t, float* count_ms, float* path_ms) {
+    if (!t) return nwi::fail(NW_ERR_ARG, "nw_table_walk_elapsed_ms: NULL table");
+    if (count_ms) *count_ms = t->walk ? t->walk->count_ms : 0.f;
+    if (path_ms) *path_ms = t->walk ? t->walk->path_ms : 0.f;
+    return NW_OK;
+}
+
+}  // extern "C"

@@ -56,7 +56,7 @@ EXPORTS = (
     "nw_table_create", "nw_table_destroy", "nw_table_set_sequences", "nw_table_fill",
     "nw_table_stats", "nw_table_elapsed_ms", "nw_table_hash", "nw_table_copy_scores",
     "nw_table_copy_codes", "nw_table_copy_last_column", "nw_table_score_pitch", "nw_table_waves",
-    "nw_table_trace",
+    "nw_table_trace", "nw_table_count_alignments", "nw_table_first_path", "nw_table_walk_elapsed_ms",
     # include/nw_panel.h
     "nw_panel_partition", "nw_panel_chain", "nw_panel_get_id", "nw_panel_create", "nw_panel_ipc_handle",
     "nw_panel_ipc_connect", "nw_panel_group_create", "nw_panel_destroy", "nw_panel_set_sequences",
@@ -147,6 +147,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "nw_panel_rows": (c_int, [c_p, P(c_i64), P(c_i64)]),
         "nw_panel_table": (c_p, [c_p]),
         "nw_panel_elapsed_ms": (c_int, [c_p, P(ctypes.c_float), P(ctypes.c_float)]),
+        "nw_table_count_alignments": (c_int, [c_p, P(c_u32)]),
+        "nw_table_first_path": (c_int, [c_p, c_p, c_i64, P(c_i64)]),
+        "nw_table_walk_elapsed_ms": (c_int, [c_p, P(ctypes.c_float), P(ctypes.c_float)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -286,6 +289,29 @@ class Table:
         if n > 0:
             self._lib.nw_table_trace(self._h, out.ctypes.data, n)
         return out.reshape(-1, 8)
+
+    def count_alignments(self) -> int:
+        """Number of optimal alignments, mod 2**32 like the reference's counter
+        (needs a fill with NW_OUT_DIRS)."""
+        c = ctypes.c_uint32()
+        _check(self._lib.nw_table_count_alignments(self._h, ctypes.byref(c)), "nw_table_count_alignments")
+        return c.value
+
+    def first_path(self) -> np.ndarray:
+        """Moves of the first alignment the reference prints (1 diag, 2 up, 4 left),
+        forward order."""
+        cap = self.L1 + self.L2
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        n = ctypes.c_int64()
+        _check(self._lib.nw_table_first_path(self._h, out.ctypes.data, cap, ctypes.byref(n)),
+               "nw_table_first_path")
+        return out[:n.value]
+
+    def walk_elapsed_ms(self):
+        a, b = ctypes.c_float(), ctypes.c_float()
+        _check(self._lib.nw_table_walk_elapsed_ms(self._h, ctypes.byref(a), ctypes.byref(b)),
+               "nw_table_walk_elapsed_ms")
+        return a.value, b.value
 
     @property
     def waves(self) -> int:
@@ -427,6 +453,34 @@ class Panel:
         a, b = ctypes.c_float(), ctypes.c_float()
         _check(self._lib.nw_panel_elapsed_ms(self._h, ctypes.byref(a), ctypes.byref(b)), "nw_panel_elapsed_ms")
         return a.value, b.value
+
+
+def render_path(s1, s2, moves) -> tuple[bytes, bytes]:
+    """Aligned (top, side) strings of a move sequence from Table.first_path()
+    (what the reference prints for that alignment, needleman-wunsch.c:296-322
+    with print_aligned_strings_and_counts, before colouring)."""
+    b1, b2 = _bytes(s1), _bytes(s2)
+    mv = np.asarray(moves, dtype=np.uint8)
+    top = np.full(len(mv), ord("-"), dtype=np.uint8)
+    side = np.full(len(mv), ord("-"), dtype=np.uint8)
+    a1 = (mv & 5) != 0            # diag or left consume s1
+    a2 = (mv & 3) != 0            # diag or up consume s2
+    if a1.sum() != len(b1) or a2.sum() != len(b2):
+        raise ValueError("moves do not span the two sequences")
+    top[a1] = np.frombuffer(b1, dtype=np.uint8)
+    side[a2] = np.frombuffer(b2, dtype=np.uint8)
+    return top.tobytes(), side.tobytes()
+
+
+def walk(s1, s2, m: int, k: int, d: int, device: int = -1):
+    """Fill (direction codes only) and walk on the device: returns
+    (optimal score, number of optimal alignments mod 2**32, (top, side) of the
+    first alignment the reference prints)."""
+    b1, b2 = _bytes(s1), _bytes(s2)
+    with Table(len(b1), len(b2), NW_OUT_DIRS, device) as t:
+        t.set_sequences(b1, b2)
+        t.fill(m, k, d, NW_OUT_DIRS)
+        return t.stats().corner, t.count_alignments(), render_path(b1, b2, t.first_path())
 
 
 # ----------------------------------------------------------------- inputs

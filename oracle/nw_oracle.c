@@ -366,3 +366,84 @@ int nwo_fill_mt(const char *s1, int64_t L1, const char *s2, int64_t L2,
         free(th);
         return 0;
 }
+
+/*
+ * Walk services over a filled code table (one byte per cell, i-major).
+ *
+ * nwo_count_paths restates the number of alignments the reference's
+ * depth-first walk reaches (construct_alignments_for_subtable,
+ * needleman-wunsch.c:209-331, counting in inc_solution_count at :250-255 with
+ * an `unsigned` counter, walk-table.c:108-147): every arrival at (0,0) is
+ * one distinct path of code edges from the corner, so the count is the
+ * path-count DP  P(0,0) = 1,  P(i,j) = [diag] P(i-1,j-1) + [left] P(i-1,j)
+ * + [up] P(i,j-1), in uint32 arithmetic (it wraps exactly like the
+ * reference's counter).
+ */
+uint32_t nwo_count_paths(const uint8_t *D, int64_t L1, int64_t L2)
+{
+        const int64_t N = L2 + 1;
+        uint32_t *prev = malloc((size_t)N * sizeof *prev);
+        uint32_t *cur = malloc((size_t)N * sizeof *cur);
+        if (!prev || !cur) {
+                free(prev);
+                free(cur);
+                return 0;
+        }
+        for (int64_t j = 0; j < N; j++) prev[j] = 1;   /* column 0: (0,0) then UP codes */
+        for (int64_t i = 1; i <= L1; i++) {
+                const uint8_t *c = D + i * N;
+                cur[0] = prev[0];                      /* (i,0): LEFT code */
+                for (int64_t j = 1; j < N; j++) {
+                        uint32_t p = 0;
+                        if (c[j] & 1) p += prev[j - 1];
+                        if (c[j] & 4) p += prev[j];
+                        if (c[j] & 2) p += cur[j - 1];
+                        cur[j] = p;
+                }
+                uint32_t *t = prev;
+                prev = cur;
+                cur = t;
+        }
+        const uint32_t r = prev[L2];
+        free(prev);
+        free(cur);
+        return r;
+}
+
+/*
+ * The first alignment the reference's walk prints: from the corner it takes
+ * the diagonal if flagged, else the left, else the up predecessor
+ * (needleman-wunsch.c:296-322), and the first arrival at (0,0) prints.
+ * moves[] receives the path in forward order ((0,0) -> (L1,L2)): 1 = diag,
+ * 2 = up (gap in s1), 4 = left (gap in s2).  Returns the number of moves, or
+ * -1 if a cell on the way has no code.
+ */
+int64_t nwo_first_path(const uint8_t *D, int64_t L1, int64_t L2, uint8_t *moves)
+{
+        const int64_t N = L2 + 1;
+        int64_t i = L1, j = L2, n = 0;
+        while (i > 0 || j > 0) {
+                const uint8_t c = D[i * N + j];
+                uint8_t mv;
+                if (c & 1) {
+                        mv = 1;
+                        i--;
+                        j--;
+                } else if (c & 4) {
+                        mv = 4;
+                        i--;
+                } else if (c & 2) {
+                        mv = 2;
+                        j--;
+                } else {
+                        return -1;
+                }
+                moves[n++] = mv;
+        }
+        for (int64_t a = 0, b = n - 1; a < b; a++, b--) {
+                const uint8_t t = moves[a];
+                moves[a] = moves[b];
+                moves[b] = t;
+        }
+        return n;
+}

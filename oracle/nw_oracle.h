@@ -70,4 +70,12 @@ int nwo_fill_mt(const char *s1, int64_t L1, const char *s2, int64_t L2,
                 int32_t m, int32_t k, int32_t d,
                 int32_t *H, uint8_t *D, nwo_stats *st, int nthreads);
 
+/* Walk services over a filled code table D (one byte per cell, i-major).
+ * nwo_count_paths: the reference's optimal-alignment count (a uint32 that
+ * wraps like its `unsigned` counter).  nwo_first_path: the first alignment the
+ * reference prints, as moves in forward order (1 diag, 2 up, 4 left);
+ * returns the move count (<= L1+L2) or -1. */
+uint32_t nwo_count_paths(const uint8_t *D, int64_t L1, int64_t L2);
+int64_t nwo_first_path(const uint8_t *D, int64_t L1, int64_t L2, uint8_t *moves);
+
 #endif

@@ -30,3 +30,8 @@ def ref_kats():
 @pytest.fixture(scope="session")
 def cli_cases():
     return load_golden("cli_cases.json")
+
+
+@pytest.fixture(scope="session")
+def walk_kats():
+    return load_golden("walk_kats.json")

@@ -15,6 +15,12 @@ Sources:
   * cli_cases.json  -- oracle/_ref/needleman-wunsch: stdout, stderr and exit
                        status of the reference CLI (needleman-wunsch.c:698-795)
                        run as `needleman-wunsch` (argv[0] matters: dbg.c:7-15).
+  * walk_kats.json   -- oracle/_ref/needleman-wunsch: the optimal-alignment
+                       count (`-q -s`, needleman-wunsch.c:250-255 via
+                       print_summary, computation.c:271-281) and the first
+                       alignment it prints (the first two stdout lines),
+                       for the walk services (nw_table_count_alignments,
+                       nw_table_first_path).
   * big_colchain.json -- 100k x 100k is beyond the reference (1.36 TB of
                        tables): produced by the clean-room restatement
                        oracle/libnworacle.so, which ref_kats.json pins against
@@ -191,9 +197,100 @@ def make_big():
     return out
 
 
+# Walk services (alignment count, first printed alignment): (kind, A, B, m, k, d).
+# Kept only when the reference's exhaustive walk finishes within WALK_TIMEOUT.
+WALK_CASES = [
+    ("str", "GCATGCU", "GATTACA", 1, 1, 1),
+    ("str", "GAT", "GTA", 1, 1, 1),
+    ("str", "GATTA", "GCAT", 2, 1, -1),
+    ("str", "ACG", "TG", 0, 0, 0),
+    ("str", "AAAA", "AA", 1, 1, 1),
+    ("str", "AAAAAAAAAA", "A", 1, 1, 1),
+    ("str", "hello,world!", "yellow~word?", 3, 2, 1),
+    ("str", "A", "ACGTACGT", 1, 1, 1),
+    ("gen", 1, 1, 1, 1, 1),
+    ("gen", 1, 50, 1, 1, 1),
+    ("gen", 50, 1, 1, 1, 1),
+    ("gen", 40, 40, 1, 1, 1),
+    ("gen", 60, 50, 1, 1, 1),
+    ("gen", 63, 65, 2, 3, 5),
+    ("gen", 64, 64, 1, 1, 1),
+    ("gen", 100, 100, 1, 1, 1),
+    ("gen", 129, 70, 2, 3, 5),
+    ("gen", 200, 200, 3, 5, 7),
+    ("gen", 150, 300, 3, 5, 7),
+    ("gen", 300, 150, 5, -4, 2),
+    ("gen", 400, 300, 5, -4, 2),
+    ("gen", 200, 200, 1, 1, -1),
+    ("gen", 250, 250, 0, 0, 0),
+]
+WALK_TIMEOUT = 20
+
+
+def make_walk():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    out = []
+    for kind, a, b, m, k, d in WALK_CASES:
+        s1, s2 = (a.encode(), b.encode()) if kind == "str" else (O.gen_dna(1, a), O.gen_dna(2, b))
+        ops = [str(m), str(k), str(d)]
+        try:
+            p = subprocess.run(["needleman-wunsch", "-q", "-s", "--"] + ops, executable=REF_CLI,
+                               input=s1 + b" " + s2 + b"\n", capture_output=True, timeout=WALK_TIMEOUT)
+        except subprocess.TimeoutExpired:
+            print("walk", kind, len(s1), len(s2), m, k, d, "reference walk too long, skipped", file=sys.stderr)
+            continue
+        err = p.stderr.decode().split("\n")
+        count = int(err[0].split()[0]) & 0xFFFFFFFF      # printed with %d from an unsigned
+        score = int(err[1].split()[-1])
+        # first printed alignment: the first two stdout lines; stop the walk there
+        q = subprocess.Popen(["needleman-wunsch", "--"] + ops, executable=REF_CLI, stdin=subprocess.PIPE,
+                             stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
+        q.stdin.write(s1 + b" " + s2 + b"\n")
+        q.stdin.close()
+        top = q.stdout.readline().rstrip(b"\n")
+        side = q.stdout.readline().rstrip(b"\n")
+        q.kill()
+        q.wait()
+        case = {"kind": kind, "m": m, "k": k, "d": d, "L1": len(s1), "L2": len(s2), "count": count,
+                "score": score, "first_top": top.decode(), "first_side": side.decode()}
+        if kind == "str":
+            case["s1"], case["s2"] = a, b
+        out.append(case)
+        print("walk", kind, len(s1), len(s2), m, k, d, count, score, file=sys.stderr)
+    return out
+
+
+def make_big_walk():
+    """100k x 100k walk services: count and first path from the restatement
+    (10 GB code table in host RAM; the oracle's walk is pinned to the reference
+    by walk_kats.json)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    out = []
+    for L1, L2, m, k, d in [(100000, 100000, 1, 1, 1)]:
+        s1, s2 = O.gen_dna(1, L1), O.gen_dna(2, L2)
+        D = np.empty((L1 + 1, L2 + 1), dtype=np.uint8)
+        st = O.Stats()
+        O.lib().nwo_fill(s1, L1, s2, L2, m, k, d, None, D.ctypes.data, ctypes.byref(st))
+        count = O.count_paths(D)
+        mv = O.first_path(D)
+        del D
+        out.append({"L1": L1, "L2": L2, "m": m, "k": k, "d": d, "corner": st.corner, "count": count,
+                    "path_len": int(len(mv)), "path_fnv": "%016x" % O.fnv(mv),
+                    "path_head": "".join("DUL"[[1, 2, 4].index(x)] for x in mv[:64].tolist()),
+                    "path_tail": "".join("DUL"[[1, 2, 4].index(x)] for x in mv[-64:].tolist()),
+                    "source": "oracle/libnworacle.so nwo_fill + nwo_count_paths + nwo_first_path "
+                              "(restatement; transitive parity via walk_kats.json)"})
+        print("big_walk", out[-1], file=sys.stderr)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true")
+    ap.add_argument("--big-walk", action="store_true", help="only the 100k walk fixture (+ the fast ones)")
     a = ap.parse_args()
     if not os.path.exists(HARNESS):
         sys.exit("build the reference first: make -C oracle ref")
@@ -201,9 +298,14 @@ def main():
         json.dump(make_kats(), f, indent=0)
     with open(os.path.join(HERE, "cli_cases.json"), "w") as f:
         json.dump(make_cli(), f, indent=1, ensure_ascii=False)
+    with open(os.path.join(HERE, "walk_kats.json"), "w") as f:
+        json.dump(make_walk(), f, indent=0)
     if a.big:
         with open(os.path.join(HERE, "big_colchain.json"), "w") as f:
             json.dump(make_big(), f, indent=1)
+    if a.big or a.big_walk:
+        with open(os.path.join(HERE, "big_walk.json"), "w") as f:
+            json.dump(make_big_walk(), f, indent=1)
 
 
 if __name__ == "__main__":

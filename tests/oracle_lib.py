@@ -44,6 +44,10 @@ def lib():
         L.nwo_gen_dna.argtypes = [ctypes.c_uint64, i64, ctypes.c_char_p]
         L.nwo_fill_band.argtypes = [ctypes.c_char_p, i64, ctypes.c_char_p, i64, i64, p, i32, i32, i32, p, p,
                                     ctypes.POINTER(Stats)]
+        L.nwo_count_paths.restype = ctypes.c_uint32
+        L.nwo_count_paths.argtypes = [p, i64, i64]
+        L.nwo_first_path.restype = i64
+        L.nwo_first_path.argtypes = [p, i64, i64, p]
         _lib = L
     return _lib
 
@@ -101,3 +105,34 @@ def kat_inputs(case):
     if case["kind"] == "str":
         return case["s1"].encode(), case["s2"].encode()
     return gen_dna(1, case["L1"]), gen_dna(2, case["L2"])
+
+
+def count_paths(D):
+    """The reference's optimal-alignment count from a code table (L1+1, L2+1)."""
+    D = np.ascontiguousarray(D, dtype=np.uint8)
+    return lib().nwo_count_paths(D.ctypes.data, D.shape[0] - 1, D.shape[1] - 1)
+
+
+def first_path(D):
+    """Moves (1 diag, 2 up, 4 left) of the first alignment the reference prints."""
+    D = np.ascontiguousarray(D, dtype=np.uint8)
+    L1, L2 = D.shape[0] - 1, D.shape[1] - 1
+    mv = np.zeros(L1 + L2 + 1, dtype=np.uint8)
+    n = lib().nwo_first_path(D.ctypes.data, L1, L2, mv.ctypes.data)
+    assert n >= 0
+    return mv[:n]
+
+
+def render_path(s1, s2, moves):
+    """Aligned (top, side) byte strings of a move sequence."""
+    X, Y = bytearray(), bytearray()
+    i = j = 0
+    for mv in moves.tolist():
+        if mv == 1:
+            X.append(s1[i]); Y.append(s2[j]); i += 1; j += 1
+        elif mv == 4:
+            X.append(s1[i]); Y.append(ord("-")); i += 1
+        else:
+            X.append(ord("-")); Y.append(s2[j]); j += 1
+    assert i == len(s1) and j == len(s2)
+    return bytes(X), bytes(Y)
