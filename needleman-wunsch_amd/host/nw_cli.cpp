@@ -109,6 +109,30 @@ int main(int argc, char** argv) {
 
     // ---- the fill (GPU) -----------------------------------------------------
     const int64_t L1 = (int64_t)strlen(s1), L2 = (int64_t)strlen(s2);
+    if (f.qflag && f.sflag && !f.lflag && !f.tflag) {
+        // `-q -s` prints only the summary (needleman-wunsch.c:667-673).  The
+        // reference gets the count by enumerating every alignment; the count
+        // is the number of code paths, computed on the device from the
+        // direction codes left in HBM -- no host tables, any size that fits.
+        nw_table* t = nullptr;
+        nw_stats st{};
+        uint32_t count = 0;
+        int rc = nw_table_create(-1, L1, L2, NW_OUT_DIRS, &t);
+        if (rc == NW_OK) rc = nw_table_set_sequences(t, s1, L1, s2, L2);
+        if (rc == NW_OK) rc = nw_table_fill(t, m, k, d, NW_OUT_DIRS);
+        if (rc == NW_OK) rc = nw_table_stats(t, &st);
+        if (rc == NW_OK) rc = nw_table_count_alignments(t, &count);
+        if (rc != NW_OK) {
+            fprintf(stderr, "%s: error: GPU fill failed: %s: %s\n", g_prog, nw_strerror(rc), nw_last_error());
+            exit(1);
+        }
+        nw_table_destroy(t);
+        nwh_print_summary(count, st.corner, stderr);
+        free(s1);
+        free(s2);
+        if (in != stdin) fclose(in);
+        return 0;
+    }
     const int64_t ncell = (L1 + 1) * (L2 + 1);
     const bool want_codes = nwh_needs_traceback(&f) || f.tflag;
     std::vector<int32_t> H;

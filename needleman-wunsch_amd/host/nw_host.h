@@ -46,6 +46,10 @@ int nwh_render(const char *s1, const char *s2, const nwh_flags *f,
                const int32_t *H, const uint8_t *codes, int32_t corner,
                int32_t gav, FILE *out, FILE *err);
 
+/* The summary print_summary() writes under -s (computation.c:271-281):
+ * "<n> optimal alignment[s]" and "Optimal score is <corner>". */
+void nwh_print_summary(unsigned solutions, int32_t corner, FILE *err);
+
 /* Same, into malloc'ed buffers (for tests); caller frees *out / *err. */
 int nwh_render_to_buffers(const char *s1, const char *s2, const nwh_flags *f,
                           const int32_t *H, const uint8_t *codes,

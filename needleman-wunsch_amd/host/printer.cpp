@@ -155,15 +155,17 @@ int nwh_render(const char* s1, const char* s2, const nwh_flags* f, const int32_t
             return -1;
         }
     }
-    if (f->sflag) {   // computation.c:271-281 (to stderr)
-        fprintf(err, "%d optimal alignment%s\n", (int)solutions, solutions > 1 ? "s" : "");
-        fprintf(err, "Optimal score is %-d\n", corner);
-    }
+    if (f->sflag) nwh_print_summary(solutions, corner, err);
     if (f->tflag) {   // needleman-wunsch.c:677-685
         if (f->qflag != 1 || f->sflag == 1 || f->lflag == 1) fputc('\n', out);
         nwh::print_table(r, walk, gav);
     }
     return 0;
+}
+
+void nwh_print_summary(unsigned solutions, int32_t corner, FILE* err) {   // computation.c:271-281
+    fprintf(err, "%d optimal alignment%s\n", (int)solutions, solutions > 1 ? "s" : "");
+    fprintf(err, "Optimal score is %-d\n", corner);
 }
 
 int nwh_render_to_buffers(const char* s1, const char* s2, const nwh_flags* f, const int32_t* H,

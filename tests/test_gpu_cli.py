@@ -33,3 +33,20 @@ def test_cli_large_summary_and_quiet():
     rc, out, err = run_cli({"args": ["-q", "-s", "1", "1", "1"], "stdin": (s1 + b" " + s2 + b"\n").decode()})
     assert rc == 0 and out == ""
     assert err == f"1 optimal alignment\nOptimal score is {st[0]}\n"
+
+
+@pytest.mark.parametrize("L1,L2,mkd", [(2000, 1500, (1, 1, 1)), (300, 250, (3, 5, 7)), (12000, 9000, (2, 3, 5))])
+def test_cli_quiet_summary_counts_random_pairs(L1, L2, mkd):
+    """`-q -s` on random pairs with exponentially many alignments: the count
+    (mod 2^32, the reference's unsigned counter) comes from the device walk
+    service; checked against the oracle's path-count DP, which
+    tests/golden/walk_kats.json pins to the reference's own enumeration."""
+    import oracle_lib as O
+    s1, s2 = O.gen_dna(5, L1), O.gen_dna(6, L2)
+    H, D, st = O.fill(s1, s2, *mkd)
+    n = O.count_paths(D)
+    n_signed = n - (1 << 32) if n >= 1 << 31 else n
+    rc, out, err = run_cli({"args": ["-q", "-s", "--"] + [str(x) for x in mkd],
+                            "stdin": (s1 + b" " + s2 + b"\n").decode()})
+    assert (rc, out) == (0, "")
+    assert err == f"{n_signed} optimal alignment{'s' if n > 1 else ''}\nOptimal score is {st[0]}\n"
