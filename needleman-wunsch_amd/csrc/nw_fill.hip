@@ -38,63 +38,15 @@
 #include <vector>
 
 #include "nw_internal.h"
+#include "nw_kern.h"
 
 namespace {
 
-constexpr int CH = 8;                 // columns per chunk (= codes per dirs word)
-#ifndef NW_XCD_DEFAULT
-#define NW_XCD_DEFAULT 0
-#endif
-constexpr int64_t SPIN_TICKS = 200000000;  // 2 s of s_memrealtime (100 MHz)
-// Panel boundary granule tags: the fill's epoch (1 .. 2^31-1), or the epoch
-// with bit 31 set when the panel above failed that fill (per-epoch, so a stale
-// poison never trips a later fill).
-constexpr uint32_t POISON_BIT = 0x80000000u;
+using namespace nwk;
 
-enum CtlWord { CTL_NEXT = 0, CTL_ABORT = 1, CTL_GAV = 2, CTL_BC = 3, CTL_ERR = 4, CTL_WORDS = 16 };
+// Ring slot (scan kernel): 8 T' of a chunk + its 8 top-string bytes (2 words).
+// In registers as the three vectors the block's wide LDS reads fill.
 
-struct FillArgs {
-    const uint8_t* s1;      // device, zero-padded to >= 8*NC + 8 bytes (s1[i-1] = column i)
-    const uint8_t* s2;      // device, zero-padded to >= 64*NG + 64 bytes
-    int32_t L1, L2;
-    int32_t m, k, d;
-    int32_t NC;             // chunks = ceil(L1 / 8)
-    int32_t NG;             // wave stripes = ceil(L2 / 64)
-    int32_t NSW;            // workgroup stripes (WG-stripes)
-    int32_t SQ, SR;         // WG-stripe k holds stripes g0 = k*SQ + min(k, SR) .. + SQ + (k < SR) - 1
-                            // (clipped to NG): the first SR WG-stripes hold one stripe more
-    int32_t* H;             // score tiles, see score_at()
-    int64_t spitch;         // 512*NC: elements per 64-row stripe
-    uint32_t* D;            // codes: word ((g*NC + q)*64 + lane)
-    int32_t* lastcol;       // score-only: H[L1][j] at lastcol[63 + j]
-    uint64_t* gran;         // boundary granules, slot s at gran + s*gpitch
-    int64_t gpitch;
-    int32_t nslot;
-    uint32_t* ctl;          // CtlWord
-    uint64_t* trace;        // optional timeline: 8 words per WG-stripe (see nw_table_trace)
-    int64_t spin_ticks;     // hand-off watchdog (s_memrealtime ticks)
-    // Row panels (multi-GPU, nw_panel.h).  The table holds global rows
-    // row_base+1 .. row_base+L2; row 0 is the boundary row of the panel above.
-    int32_t row_base;
-    uint32_t epoch;         // tag of this fill's panel hand-off granules
-    const uint64_t* xin;    // top boundary row {epoch, H-d} per column, or null (= seeded row 0)
-    uint64_t* xout;         // bottom row granules for the panel below, or null
-    uint32_t* xflag;        // host-visible: xflag[b] = epoch once block b of xout is written
-    int32_t xblk;           // chunks per block
-    int32_t xcd_map;        // 1: one WG-stripe per block, consecutive WG-stripes on blocks of one XCD
-};
-
-// ---------------------------------------------------------------- DPP helpers
-typedef const __attribute__((address_space(4))) uint64_t* cptr64;
-
-
-// LDS byte address of a __shared__ object (for ds_* in inline asm).
-__device__ __forceinline__ int lds_addr(const void* p) {
-    return (int)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// Wave-uniform copies of per-wave values (so address math stays scalar).
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // ------------------------------------------------------------ column steps
 // Domain.  A wave works on G' = H + r*d + (i - base)*d, r = row offset inside
@@ -106,16 +58,7 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 //     sub' = match ? m + 2d : 2d - k,   T'_i = the row above, same domain.
 // base moves every 512 chunks so |G'| stays within |H| + (64W + 4104)|d|.
 // Cell recurrence = needleman-wunsch.c:429-465; direction flags :485-503.
-constexpr int SUPER_CHUNKS = 512;     // chunks per super-chunk (4096 columns)
 
-__device__ __forceinline__ int chunk_base(int c) { return (c / SUPER_CHUNKS) * (SUPER_CHUNKS * CH); }
-
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v2i __attribute__((ext_vector_type(2)));
-
-// Ring slot: 8 T' of a chunk + its 8 top-string bytes (2 words), 16-int stride.
-// In registers as the three vectors the block's wide LDS reads fill.
-constexpr int SLOT = 16;
 struct RingSlot {
     v4i a, b;           // T' of steps 0..3, 4..7
     v2i c;              // top-string bytes of columns 1..4, 5..8 of the chunk
@@ -237,23 +180,6 @@ __device__ __forceinline__ void store_chunk_scores(const ChunkRegs& r, const Chu
 }
 #endif
 
-// Hand-off granule load: agent scope between workgroups of one fill, system
-// scope (bypassing L2) for the panel boundary, which another agent writes.
-__device__ __forceinline__ uint64_t ld_gran(const uint64_t* p, bool sys) {
-    return sys ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-               : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// LDS counters of the barrier-free intra-workgroup pipeline.
-__device__ __forceinline__ int lds_ld(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_publish(int* p, int v) {
-    // Every LDS write this wave issued before (ring data) lands first: the
-    // LDS executes one wave's DS instructions in order, so a reader that sees
-    // the counter and then reads the ring sees the data.
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 // Workgroup = W compute waves (64-row stripes, stacked) + 1 loader wave, no
 // barriers inside a stripe.  Wave w takes the top row of each 8-column chunk
@@ -620,7 +546,8 @@ struct TableView {
     const int32_t* tiles;   // score tiles
     int64_t spitch;
     const uint32_t* D;      // codes, or null
-    int32_t NC;
+    int32_t NC;             // chunks per stripe of the layout (scan: ceil(L1/8); skew: ceil((L1+63)/8))
+    int32_t skew;           // 1: skewed layout (nw_skew.inc), 0: column layout (scan kernel)
     int32_t d;
     int32_t row_base;       // panels: global row of local row 0
     const uint64_t* top;    // panels: boundary row granules (H - d), or null for row 0 = seed
@@ -634,7 +561,10 @@ struct TableView {
 // column i = 4q + r + 1 at g*spitch + (q*64 + l)*4 + r, so a lane's 4
 // consecutive columns are one 16-byte store and a chunk is 2 KB contiguous.
 // Column tiles: g*spitch + (i-1)*64 + l, one 256-byte store per column.
-__host__ __device__ __forceinline__ int64_t score_index(int64_t r, int64_t c, int64_t spitch) {
+// Skewed layout (nw_skew.inc): stored by step t = c + (r & 63) instead of
+// by column, same quad tiles.
+__host__ __device__ __forceinline__ int64_t score_index(int64_t r, int64_t c, int64_t spitch, bool skew = false) {
+    if (skew) c += r & 63;
 #if NW_SCORE_X4
     return (r >> 6) * spitch + ((c >> 2) * 64 + (r & 63)) * 4 + (c & 3);
 #else
@@ -642,10 +572,18 @@ __host__ __device__ __forceinline__ int64_t score_index(int64_t r, int64_t c, in
 #endif
 }
 
+// Code word and bit position of interior cell (i, j) (see include/nw_fill.h).
+__host__ __device__ __forceinline__ int64_t code_word(int64_t i, int64_t j, int64_t NC, bool skew, int* shift) {
+    const int64_t g = (j - 1) >> 6, l = (j - 1) & 63;
+    const int64_t t = (i - 1) + (skew ? l : 0);
+    *shift = 21 - 3 * (int)(t & 7);
+    return (g * (NC + 1) + (t >> 3) + 1) * 64 + l;
+}
+
 __device__ __forceinline__ int32_t score_at(const TableView& v, int64_t i, int64_t j) {
     if (i == 0) return (int32_t)(-(j + v.row_base) * (int64_t)v.d);
     if (j == 0) return v.top ? (int32_t)(uint32_t)v.top[i - 1] + v.d : (int32_t)(-i * (int64_t)v.d);
-    return v.tiles[score_index(j - 1, i - 1, v.spitch)];
+    return v.tiles[score_index(j - 1, i - 1, v.spitch, v.skew)];
 }
 
 // Dense i-major copy of columns [i0, i1): out[(i-i0)*(L2+1) + j].
@@ -663,8 +601,9 @@ __device__ __forceinline__ uint32_t code_at(const TableView& v, int64_t i, int64
     if (j == 0 && v.row_base > 0) return 0u;
     if (i == 0) return j == 0 ? 0u : 2u;          // (0,0): none; (0,j): up
     if (j == 0) return 4u;                         // (i,0): left
-    const int64_t g = (j - 1) >> 6, l = (j - 1) & 63, q = (i - 1) >> 3, s = (i - 1) & 7;
-    return (v.D[(g * (v.NC + 1) + q + 1) * 64 + l] >> (21 - 3 * s)) & 7u;
+    int sh;
+    const int64_t wd = code_word(i, j, v.NC, v.skew, &sh);
+    return (v.D[wd] >> sh) & 7u;
 }
 
 // Dense nibble packing for nw_fill(): byte b = code(2b) | code(2b+1) << 4.
@@ -709,7 +648,6 @@ __global__ void nw_colhash_kernel(TableView v, int32_t L1, int32_t L2, uint64_t*
 }
 
 // --------------------------------------------------------------- host side
-using KernelFn = void (*)(FillArgs);
 
 template <int W, bool P>
 KernelFn pick_flags(bool sh, bool sd, bool stt) {
@@ -774,7 +712,8 @@ TableView view_of(const nw_table* t) {
     v.tiles = t->H;
     v.spitch = t->spitch;
     v.D = (t->last_mask & NW_OUT_DIRS) ? t->D : nullptr;
-    v.NC = (int32_t)t->NC;
+    v.NC = (int32_t)t->lay_NC;
+    v.skew = t->skew;
     v.d = t->last_d;
     v.row_base = (int32_t)t->row_base;
     v.top = t->row_base > 0 ? t->xin : nullptr;
@@ -816,6 +755,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
     NW_HIPCHK(hipEventRecord(t->ev[0], t->stream));
     NW_HIPCHK(hipMemsetAsync(t->ctl, 0, CTL_WORDS * 4, t->stream));
     int W = 0;
+    bool skew = false;
     if (L1 > 0 && L2 > 0) {
         const StripePlan plan = plan_stripes(t->NG, t->ncu);
         W = plan.W;
@@ -825,8 +765,22 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         const char* pe = getenv("NW_PROF");
         const bool prof = t->alpha > 0 && vcm >= -128 && vcm <= 127 && vck >= -128 && vck <= 127 &&
                           !(pe && atoi(pe) == 0);
-        KernelFn fn = pick_kernel(W, prof, sh, sd, stt);
+        // Kernel: the column scan (nw_fill_kernel) or the skewed-stripe
+        // wavefront (nw_skew.hip); they write different tile layouts
+        // (TableView.skew).  The skew kernel's critical path is L1 + 72*NG
+        // steps of ~110 cycles, the scan's L1 steps of ~150-230 cycles plus
+        // ~1.2 us per stripe, so the skew kernel wins only on wide tables with
+        // few stripes (measured: 1M x 20k 61 vs 75 ms, 100k x 64 4.6 vs
+        // 6.2 ms; 100k x 100k 22 vs 11 ms).  $NW_KERNEL = scan |
+        // skew | auto (default).
+        const char* ke = getenv("NW_KERNEL");
+        if (ke && std::strcmp(ke, "skew") == 0) skew = true;
+        else if (ke && std::strcmp(ke, "scan") == 0) skew = false;
+        else skew = t->NG <= 4 * (int64_t)t->ncu && L1 >= 4 * L2;
+        KernelFn fn = skew ? pick_skew(W, prof, sh, sd, stt) : pick_kernel(W, prof, sh, sd, stt);
         if (!fn) return fail(NW_ERR_ARG, "nw_table_fill: unsupported wave count");
+        const int64_t NCH = skew ? (L1 + 63 + CH - 1) / CH : t->NC;
+        t->spitch = 512 * NCH;
         FillArgs a{};
         a.s1 = t->s1;
         a.s2 = t->s2;
@@ -836,6 +790,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         a.k = k;
         a.d = d;
         a.NC = (int32_t)t->NC;
+        a.NCH = (int32_t)NCH;
         a.NG = (int32_t)t->NG;
         a.NSW = (int32_t)plan.NSW;
         a.SQ = plan.SQ;
@@ -881,7 +836,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         // neighbours' kernels share the CUs).
         {
             const char* e = getenv("NW_XCD");
-            a.xcd_map = (!panel && grid == a.NSW && (e ? atoi(e) != 0 : NW_XCD_DEFAULT)) ? 1 : 0;
+            a.xcd_map = (!skew && !panel && grid == a.NSW && (e ? atoi(e) != 0 : NW_XCD_DEFAULT)) ? 1 : 0;
         }
         a.nslot = (int32_t)std::min<int64_t>(grid + 1, (int64_t)(t->gran_bytes / 8 / a.gpitch));
         if (a.nslot < grid + 1) return fail(NW_ERR_ARG, "nw_table_fill: granule buffer too small");
@@ -900,6 +855,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
     t->pend_mask = out_mask;
     t->pend_d = d;
     t->pend_W = W;
+    t->pend_skew = skew;
     return NW_OK;
 }
 
@@ -923,7 +879,7 @@ int fill_finish(nw_table* t) {
     int32_t corner = 0;
     if (L1 > 0 && L2 > 0) {
         const int64_t r = L2 - 1, q = L1 - 1;
-        const int32_t* src = sh ? t->H + score_index(r, q, t->spitch) : t->lastcol + L2;
+        const int32_t* src = sh ? t->H + score_index(r, q, t->spitch, t->pend_skew) : t->lastcol + L2;
         NW_HIPCHK(hipMemcpyAsync(&corner, src, 4, hipMemcpyDeviceToHost, t->stream));
     }
     NW_HIPCHK(hipStreamSynchronize(t->stream));
@@ -941,6 +897,8 @@ int fill_finish(nw_table* t) {
     t->last_mask = t->pend_mask;
     t->last_d = d;
     t->waves = t->pend_W;
+    t->skew = t->pend_skew;
+    t->lay_NC = t->spitch / 512;
     return NW_OK;
 }
 
@@ -1032,11 +990,11 @@ int nw_table_create(int device, int64_t max_L1, int64_t max_L2, uint32_t out_mas
     if ((rc = alloc((void**)&t->s1, (size_t)(CH * NC + 64)))) return bail(rc);
     if ((rc = alloc((void**)&t->s2, (size_t)(64 * NG + 1024)))) return bail(rc);
     if (out_mask & NW_OUT_SCORES) {
-        if ((rc = alloc((void**)&t->H, (size_t)std::max<int64_t>(NG, 1) * (size_t)std::max<int64_t>(NC, 1) * 2048)))
+        if ((rc = alloc((void**)&t->H, (size_t)std::max<int64_t>(NG, 1) * (size_t)(NC + 8) * 2048)))
             return bail(rc);
     }
     if (out_mask & NW_OUT_DIRS) {
-        if ((rc = alloc((void**)&t->D, (size_t)std::max<int64_t>(NG, 1) * (NC + 1) * 256))) return bail(rc);
+        if ((rc = alloc((void**)&t->D, (size_t)std::max<int64_t>(NG, 1) * (NC + 9) * 256))) return bail(rc);
     }
     if ((rc = alloc((void**)&t->lastcol, (size_t)(64 * NG + 128) * 4))) return bail(rc);
     // Granule slots: one per concurrently running WG-stripe + 1.

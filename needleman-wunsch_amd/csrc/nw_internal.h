@@ -19,7 +19,9 @@ struct nw_table {
     int64_t max_L1 = 0, max_L2 = 0;
     // geometry for the current sequences
     int64_t L1 = -1, L2 = -1;
-    int64_t NC = 0, NG = 0, spitch = 0;
+    int64_t NC = 0, NG = 0, spitch = 0;   // NC = ceil(L1/8) column chunks; spitch: see fill_launch
+    int skew = 0;                   // layout of the tables: 1 = skewed (nw_skew.inc), 0 = column (scan)
+    int64_t lay_NC = 0;             // chunks per stripe of that layout
     int alpha = 0;                  // s1/s2 coded to symbols 0..alpha-1 on the device (<= 8), 0: raw bytes
     // device buffers
     uint8_t* s1 = nullptr;
@@ -45,6 +47,7 @@ struct nw_table {
     uint32_t pend_mask = 0;
     int32_t pend_d = 0;
     int pend_W = 0;
+    int pend_skew = 0;
     // results of the last fill
     bool filled = false;
     uint32_t last_mask = 0;

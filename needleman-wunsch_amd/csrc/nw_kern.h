@@ -1,0 +1,103 @@
+// nw_kern.h -- definitions shared by the fill kernels (nw_fill.hip: the
+// column-scan kernel; nw_skew.hip: the skewed-stripe kernel) and their
+// launcher.  Device-side only; not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "nw_internal.h"
+
+namespace nwk {
+
+constexpr int CH = 8;                 // columns per chunk (= codes per dirs word)
+#ifndef NW_XCD_DEFAULT
+#define NW_XCD_DEFAULT 0
+#endif
+constexpr int64_t SPIN_TICKS = 200000000;  // 2 s of s_memrealtime (100 MHz)
+// Panel boundary granule tags: the fill's epoch (1 .. 2^31-1), or the epoch
+// with bit 31 set when the panel above failed that fill (per-epoch, so a stale
+// poison never trips a later fill).
+constexpr uint32_t POISON_BIT = 0x80000000u;
+
+enum CtlWord { CTL_NEXT = 0, CTL_ABORT = 1, CTL_GAV = 2, CTL_BC = 3, CTL_ERR = 4, CTL_WORDS = 16 };
+
+struct FillArgs {
+    const uint8_t* s1;      // device, zero-padded to >= 8*NC + 8 bytes (s1[i-1] = column i)
+    const uint8_t* s2;      // device, zero-padded to >= 64*NG + 64 bytes
+    int32_t L1, L2;
+    int32_t m, k, d;
+    int32_t NC;             // chunks = ceil(L1 / 8) (ring slots / granule chunks)
+    int32_t NCH;            // skew kernel: 8-step chunks per stripe = ceil((L1 + 63) / 8)
+    int32_t NG;             // wave stripes = ceil(L2 / 64)
+    int32_t NSW;            // workgroup stripes (WG-stripes)
+    int32_t SQ, SR;         // WG-stripe k holds stripes g0 = k*SQ + min(k, SR) .. + SQ + (k < SR) - 1
+                            // (clipped to NG): the first SR WG-stripes hold one stripe more
+    int32_t* H;             // score tiles, see score_at()
+    int64_t spitch;         // 512*NC: elements per 64-row stripe
+    uint32_t* D;            // codes: word ((g*NC + q)*64 + lane)
+    int32_t* lastcol;       // score-only: H[L1][j] at lastcol[63 + j]
+    uint64_t* gran;         // boundary granules, slot s at gran + s*gpitch
+    int64_t gpitch;
+    int32_t nslot;
+    uint32_t* ctl;          // CtlWord
+    uint64_t* trace;        // optional timeline: 8 words per WG-stripe (see nw_table_trace)
+    int64_t spin_ticks;     // hand-off watchdog (s_memrealtime ticks)
+    // Row panels (multi-GPU, nw_panel.h).  The table holds global rows
+    // row_base+1 .. row_base+L2; row 0 is the boundary row of the panel above.
+    int32_t row_base;
+    uint32_t epoch;         // tag of this fill's panel hand-off granules
+    const uint64_t* xin;    // top boundary row {epoch, H-d} per column, or null (= seeded row 0)
+    uint64_t* xout;         // bottom row granules for the panel below, or null
+    uint32_t* xflag;        // host-visible: xflag[b] = epoch once block b of xout is written
+    int32_t xblk;           // chunks per block
+    int32_t xcd_map;        // 1: one WG-stripe per block, consecutive WG-stripes on blocks of one XCD
+};
+
+// ---------------------------------------------------------------- DPP helpers
+typedef const __attribute__((address_space(4))) uint64_t* cptr64;
+
+
+// LDS byte address of a __shared__ object (for ds_* in inline asm).
+__device__ __forceinline__ int lds_addr(const void* p) {
+    return (int)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// Wave-uniform copies of per-wave values (so address math stays scalar).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+constexpr int SUPER_CHUNKS = 512;     // chunks per super-chunk (4096 columns)
+
+__device__ __forceinline__ int chunk_base(int c) { return (c / SUPER_CHUNKS) * (SUPER_CHUNKS * CH); }
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v2i __attribute__((ext_vector_type(2)));
+
+// Ring slot stride (ints): 8 values of a chunk (+ the scan kernel's 8 top-string bytes).
+constexpr int SLOT = 16;
+
+// Hand-off granule load: agent scope between workgroups of one fill, system
+// scope (bypassing L2) for the panel boundary, which another agent writes.
+__device__ __forceinline__ uint64_t ld_gran(const uint64_t* p, bool sys) {
+    return sys ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+               : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// LDS counters of the barrier-free intra-workgroup pipeline.
+__device__ __forceinline__ int lds_ld(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_publish(int* p, int v) {
+    // Every LDS write this wave issued before (ring data) lands first: the
+    // LDS executes one wave's DS instructions in order, so a reader that sees
+    // the counter and then reads the ring sees the data.
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+using KernelFn = void (*)(FillArgs);
+
+// nw_skew.hip: the skewed-stripe kernel for W compute waves per workgroup
+// (nullptr for an unsupported W).
+KernelFn pick_skew(int W, bool prof, bool sh, bool sd, bool stt);
+
+}  // namespace nwk

@@ -48,7 +48,8 @@ constexpr uint32_t POISON = 0x80000000u;
 
 struct CountArgs {
     const uint32_t* D;    // codes, include/nw_fill.h layout
-    int64_t NC;           // 8-column chunks of the current L1
+    int64_t NC;           // 8-step chunks per stripe of the table's layout
+    int32_t skew;         // skewed layout: lane l's word index runs ahead by l steps
     int32_t L1, L2, NG;
     uint64_t* rows;       // granule (g, i) at g*L1 + i-1: P(i, 64(g+1)) for stripe g < NG-1
     uint32_t* ctl;
@@ -80,7 +81,9 @@ __global__ __launch_bounds__(64) void nw_count_kernel(CountArgs a) {
         uint64_t* bot = g < a.NG - 1 ? a.rows + (int64_t)g * a.L1 : nullptr;
         uint32_t P = 1;         // column 0: (0,j) has only the up code, P = 1
         uint32_t Tprev = 1;     // P(0, 64g)
-        uint32_t w = 0, wn = a.NC > 0 ? Dg[0] : 0u;
+        // this lane's step of column i is t = i - 1 (+ lane in the skewed layout)
+        const int toff = a.skew ? lane : 0;
+        uint32_t w = 0, wn = a.NC > 0 ? Dg[(int64_t)(toff >> 3) * 64] : 0u;
         bool dead = false;
         for (int i0 = 1; i0 <= a.L1 && !dead; i0 += CBLK) {
             const int cnt = min(CBLK, a.L1 - i0 + 1);
@@ -112,10 +115,11 @@ __global__ __launch_bounds__(64) void nw_count_kernel(CountArgs a) {
             uint32_t outv = 0;
             for (int c = 0; c < cnt; ++c) {
                 const int i = i0 + c;
-                const int s = (i - 1) & 7;
-                if (s == 0) {
+                const int t = i - 1 + toff;
+                const int s = t & 7;
+                if (s == 0 || i == 1) {
                     w = wn;
-                    const int64_t qn = ((i - 1) >> 3) + 1;
+                    const int64_t qn = (t >> 3) + 1;
                     if (qn < a.NC) wn = Dg[qn * 64];
                 }
                 const uint32_t code = (w >> (21 - 3 * s)) & 7u;
@@ -152,8 +156,8 @@ __global__ __launch_bounds__(64) void nw_count_kernel(CountArgs a) {
 
 // Greedy walk diag > left > up from (L1, L2) to (0, 0).  Moves are written
 // back to front; ctl[3] = count, ctl[4] = 1 if a cell had no code.
-__global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, int64_t NC, int32_t L1, int32_t L2,
-                                                           uint8_t* moves, uint32_t* ctl) {
+__global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, int64_t NC, int32_t skew, int32_t L1,
+                                                           int32_t L2, uint8_t* moves, uint32_t* ctl) {
     __shared__ uint32_t blk[8][64];
     const int lane = threadIdx.x;
     int i = L1, j = L2;
@@ -162,7 +166,8 @@ __global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, in
     int64_t qb = -1;
     while (i > 0 && j > 0) {
         const int g = (j - 1) >> 6;
-        const int64_t q = (i - 1) >> 3, q0 = q & ~(int64_t)7;
+        const int64_t t = (i - 1) + (skew ? ((j - 1) & 63) : 0);   // step of (i, j) in its stripe
+        const int64_t q = t >> 3, q0 = q & ~(int64_t)7;
         if (g != gb || q0 != qb) {
             __syncthreads();
 #pragma unroll
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, in
             gb = g;
             qb = q0;
         }
-        const uint32_t code = (blk[q - q0][(j - 1) & 63] >> (21 - 3 * ((i - 1) & 7))) & 7u;
+        const uint32_t code = (blk[q - q0][(j - 1) & 63] >> (21 - 3 * (int)(t & 7))) & 7u;
         uint8_t mv;
         if (code & 1u) {
             mv = 1;
@@ -257,7 +262,8 @@ int nw_table_count_alignments(nw_table* t, uint32_t* count) {
     if (++w->epoch & POISON) w->epoch = 1;   // tags stay below the poison bit
     CountArgs a{};
     a.D = t->D;
-    a.NC = t->NC;
+    a.NC = t->lay_NC;
+    a.skew = t->skew;
     a.L1 = (int32_t)t->L1;
     a.L2 = (int32_t)t->L2;
     a.NG = (int32_t)NG;
@@ -297,7 +303,8 @@ int nw_table_first_path(nw_table* t, uint8_t* moves, int64_t cap, int64_t* n) {
     }
     NW_HIPCHK(hipMemsetAsync(w->ctl, 0, 64, t->stream));
     NW_HIPCHK(hipEventRecord(t->ev[2], t->stream));
-    nw_first_path_kernel<<<1, 64, 0, t->stream>>>(t->D, t->NC, (int32_t)t->L1, (int32_t)t->L2, w->moves, w->ctl);
+    nw_first_path_kernel<<<1, 64, 0, t->stream>>>(t->D, t->lay_NC, t->skew, (int32_t)t->L1, (int32_t)t->L2, w->moves,
+                                                  w->ctl);
     NW_HIPCHK(hipGetLastError());
     NW_HIPCHK(hipEventRecord(t->ev[3], t->stream));
     uint32_t ctl[8];

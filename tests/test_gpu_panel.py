@@ -19,6 +19,14 @@ import nw_amd
 import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
+
+@pytest.fixture(params=["scan", "skew"], autouse=True)
+def fill_kernel(request, monkeypatch):
+    """Every test runs on both fill kernels (nw_fill.hip's column scan and
+    nw_skew.hip's skewed stripes), which write different device layouts."""
+    monkeypatch.setenv("NW_KERNEL", request.param)
+    return request.param
+
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 
 

@@ -17,6 +17,14 @@ import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
 
+@pytest.fixture(params=["scan", "skew"], autouse=True)
+def fill_kernel(request, monkeypatch):
+    """Every test runs on both fill kernels (nw_fill.hip's column scan and
+    nw_skew.hip's skewed stripes), which write different device layouts."""
+    monkeypatch.setenv("NW_KERNEL", request.param)
+    return request.param
+
+
 DIRS = nw_amd.NW_OUT_DIRS
 
 
