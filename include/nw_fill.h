@@ -169,6 +169,18 @@ int nw_table_count_alignments(nw_table *t, uint32_t *count);
  * 2 = up (gap over s2[j]), 4 = left (s1[i] over a gap).  cap >= L1 + L2. */
 int nw_table_first_path(nw_table *t, uint8_t *moves, int64_t cap, int64_t *n);
 
+/* nw_first_path_banded: nw_table_first_path's result without the full
+ * table, for pairs whose direction codes do not fit (or are not wanted) in
+ * device memory: a score-only forward pass keeps one boundary row per band of
+ * band_rows rows (a multiple of 64), then the bands are refilled with codes
+ * bottom-up and walked greedily (needleman-wunsch.c:296-322), each only left
+ * of where the walk entered it.  Device memory ~ band_rows * L1 / 2 bytes +
+ * 8 * L1 per band; time ~ two fills.  Not in the reference (its traceback
+ * needs every cell's walk state, walk-table.c:58-79); SURVEY.md 8(f) item 3.
+ * device: as nw_fill; cap >= L1 + L2; moves as nw_table_first_path. */
+int nw_first_path_banded(int device, const char *s1, int64_t L1, const char *s2, int64_t L2,
+                         int32_t m, int32_t k, int32_t d, int64_t band_rows,
+                         uint8_t *moves, int64_t cap, int64_t *n);
 /* Device time (ms) of the last count / first-path kernel (HIP events). */
 int nw_table_walk_elapsed_ms(nw_table *t, float *count_ms, float *path_ms);
 

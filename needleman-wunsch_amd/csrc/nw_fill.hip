@@ -270,11 +270,31 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             const uint32_t want = xsrc ? a.epoch : (uint32_t)sidx;
             const uint32_t* s1w = reinterpret_cast<const uint32_t*>(a.s1);
             const bool chl = lane == 8 || lane == 9;
-            uint64_t pf = 0;
+            // Granule window: lane l holds granule (cw + l/8, column l%8), so
+            // one load covers 8 chunks and pn prefetches the next 8; a poll
+            // reloads only the lanes of chunks >= c that are not valid yet.
+            // (One chunk per load round trip made the loader, not the
+            // producer, pace a WG-stripe behind its predecessor.)
+            const int wk = lane >> 3, wb = lane & 7;
+            const int64_t ngr = (int64_t)CH * NC;
+            auto gload = [&](int cf) -> uint64_t {
+                const int64_t x = (int64_t)CH * cf + lane;
+                return x < ngr ? ld_gran(gin + x, xsrc) : 0ull;
+            };
+            int cw = 0;
+            uint64_t pf = 0, pn = 0;
             uint32_t pc = chl ? s1w[lane - 8] : 0u;
-            if (!seeded && lane < CH) pf = ld_gran(gin + lane, xsrc);
+            if (!seeded) {
+                pf = gload(0);
+                pn = gload(CH);
+            }
             for (int c = 0; c < NC; ++c) {
                 const int n = (c == NC - 1) ? nlast : CH;
+                if (c == cw + CH) {
+                    cw += CH;
+                    pf = pn;
+                    if (!seeded) pn = gload(cw + CH);
+                }
                 while (lds_ld(&ctr[1]) < c - R + 1) __builtin_amdgcn_s_sleep(1);   // ring slot free?
                 int* dst = &tring[(c % R) * SLOT];
                 const int base = chunk_base(c);
@@ -282,19 +302,20 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
                     // row 0: H[i][0] - d = -(i+1)*d (computation.c:102-110) -> G' = -(base+1)*d
                     if (lane < CH) dst[lane] = -(base + 1) * d;
                 } else {
-                    bool ok = lane >= n || (uint32_t)(pf >> 32) == want;
+                    const bool mine = wk == c - cw;           // this lane carries chunk c
+                    bool ok = !mine || wb >= n || (uint32_t)(pf >> 32) == want;
                     if (!__all(ok)) {
                         const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
                         for (;;) {
                             __builtin_amdgcn_s_sleep(1);
-                            if (!ok) pf = ld_gran(gin + CH * (int64_t)c + lane, xsrc);
-                            ok = lane >= n || (uint32_t)(pf >> 32) == want;
+                            if (wk >= c - cw && (uint32_t)(pf >> 32) != want) pf = gload(cw);
+                            ok = !mine || wb >= n || (uint32_t)(pf >> 32) == want;
                             if (__all(ok)) break;
                             const int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
                             const uint32_t ab = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED,
                                                                   __HIP_MEMORY_SCOPE_AGENT);
                             // a failed panel above poisons its boundary row
-                            const bool peer = xsrc && __any(lane < n && (uint32_t)(pf >> 32) == (want | POISON_BIT));
+                            const bool peer = xsrc && __any(mine && wb < n && (uint32_t)(pf >> 32) == (want | POISON_BIT));
                             if (ab || peer || now - t0 > a.spin_ticks) {
                                 if (lane == 0) {
                                     __hip_atomic_store(&a.ctl[CTL_ABORT], 1u, __ATOMIC_RELAXED,
@@ -310,9 +331,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
                     }
                     if (lds_ld(&sh_abort)) break;
                     // H - d of the row above -> G' of lane -1: + (i - base)*d
-                    if (lane < CH) dst[lane] = (int)(uint32_t)pf + (CH * c + lane + 1 - base) * d;
-                    if (c + 1 < NC && lane < CH)          // prefetch the next chunk
-                        pf = ld_gran(gin + CH * (int64_t)(c + 1) + lane, xsrc);
+                    if (mine) dst[wb] = (int)(uint32_t)pf + (CH * c + wb + 1 - base) * d;
                 }
                 if (chl) {
                     dst[lane] = (int)pc;

@@ -154,13 +154,17 @@ __global__ __launch_bounds__(64) void nw_count_kernel(CountArgs a) {
     }
 }
 
-// Greedy walk diag > left > up from (L1, L2) to (0, 0).  Moves are written
-// back to front; ctl[3] = count, ctl[4] = 1 if a cell had no code.
-__global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, int64_t NC, int32_t skew, int32_t L1,
-                                                           int32_t L2, uint8_t* moves, uint32_t* ctl) {
+// Greedy walk diag > left > up from (i0, j0) (the corner for a whole
+// table).  Moves are written back to front; ctl[3] = count, ctl[4] = 1 if a
+// cell had no code, ctl[5] = the column where the walk left through row 0.
+// top = 1: row 0 is the seeded first row, so the walk runs on along row 0 /
+// column 0 to (0, 0); top = 0 (a band of rows below another): it stops on
+// row 0, which is the band above's last row.
+__global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, int64_t NC, int32_t skew, int32_t i0,
+                                                           int32_t j0, int32_t top, uint8_t* moves, uint32_t* ctl) {
     __shared__ uint32_t blk[8][64];
     const int lane = threadIdx.x;
-    int i = L1, j = L2;
+    int i = i0, j = j0;
     uint32_t n = 0;
     int gb = -1;
     int64_t qb = -1;
@@ -198,9 +202,13 @@ __global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, in
     }
     for (; j > 0; --j, ++n)      // column 0: up codes
         if (lane == 0) moves[n] = 2;
-    for (; i > 0; --i, ++n)      // row 0: left codes
-        if (lane == 0) moves[n] = 4;
-    if (lane == 0) ctl[3] = n;
+    if (top)
+        for (; i > 0; --i, ++n)  // row 0: left codes
+            if (lane == 0) moves[n] = 4;
+    if (lane == 0) {
+        ctl[3] = n;
+        ctl[5] = (uint32_t)i;
+    }
 }
 
 int check_walkable(nw_table* t, const char* who) {
@@ -303,7 +311,7 @@ int nw_table_first_path(nw_table* t, uint8_t* moves, int64_t cap, int64_t* n) {
     }
     NW_HIPCHK(hipMemsetAsync(w->ctl, 0, 64, t->stream));
     NW_HIPCHK(hipEventRecord(t->ev[2], t->stream));
-    nw_first_path_kernel<<<1, 64, 0, t->stream>>>(t->D, t->lay_NC, t->skew, (int32_t)t->L1, (int32_t)t->L2, w->moves,
+    nw_first_path_kernel<<<1, 64, 0, t->stream>>>(t->D, t->lay_NC, t->skew, (int32_t)t->L1, (int32_t)t->L2, 1, w->moves,
                                                   w->ctl);
     NW_HIPCHK(hipGetLastError());
     NW_HIPCHK(hipEventRecord(t->ev[3], t->stream));
@@ -328,6 +336,111 @@ int nw_table_walk_elapsed_ms(nw_table* t, float* count_ms, float* path_ms) {
     if (count_ms) *count_ms = t->walk ? t->walk->count_ms : 0.f;
     if (path_ms) *path_ms = t->walk ? t->walk->path_ms : 0.f;
     return NW_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Banded checkpoint traceback: the first alignment the
+// reference prints, for pairs whose full direction table does not fit.
+//
+//   1. Forward: the rows are cut into bands of `band_rows` (a multiple of 64).
+//      Bands 0 .. K-2 are filled score-only, one after the other, each taking
+//      its top row from the band above and handing its bottom row to the band
+//      below through the panel boundary granules {epoch, H - d}
+//      (fill_launch's xin / xout) -- K-1 rows of L1 granules are all that is
+//      kept.
+//   2. Backward: band K-1 .. 0 is refilled with direction codes (only columns
+//      1 .. i_entry: a walk that entered at column i_entry never goes right)
+//      and walked greedily diag > left > up from its entry cell until it
+//      leaves through the band's top row; the exit column is the next band's
+//      entry.  The greedy order is the reference's print order
+//      (needleman-wunsch.c:296-322), so the result is nw_table_first_path's.
+// Device memory: band_rows x L1 direction codes (0.5 B per cell) + the K-1
+// boundary rows; time: about two fills of the table.
+int nw_first_path_banded(int device, const char* s1, int64_t L1, const char* s2, int64_t L2, int32_t m, int32_t k,
+                         int32_t d, int64_t band_rows, uint8_t* moves, int64_t cap, int64_t* n) {
+    if (L1 < 0 || L2 < 0 || (L1 && !s1) || (L2 && !s2) || !n || cap < L1 + L2 || (cap > 0 && !moves) ||
+        band_rows < 64 || band_rows % 64 != 0 || L1 > INT32_MAX - 64 || L2 > INT32_MAX - 4096)
+        return nwi::fail(NW_ERR_ARG, "nw_first_path_banded: bad arguments (band_rows: a positive multiple of 64)");
+    *n = 0;
+    if (L1 == 0 || L2 == 0) {   // the seeded row / column
+        for (int64_t x = 0; x < L2; ++x) moves[x] = 2;
+        for (int64_t x = 0; x < L1; ++x) moves[L2 + x] = 4;
+        *n = L1 + L2;
+        return NW_OK;
+    }
+    const int64_t K = (L2 + band_rows - 1) / band_rows;
+    const int64_t rows_max = std::min(band_rows, L2);
+    nw_table* t = nullptr;
+    int rc = nw_table_create(device, L1, rows_max, NW_OUT_DIRS, &t);
+    if (rc) return rc;
+    uint64_t* rows = nullptr;   // boundary b (below band b): rows[b * L1 ..]
+    uint32_t* ctl = nullptr;
+    uint8_t* dmoves = nullptr;
+    std::vector<uint8_t> path;  // back to front
+    path.reserve((size_t)(L1 + L2));
+    auto done = [&](int r) {
+        (void)hipFree(rows);
+        (void)hipFree(ctl);
+        (void)hipFree(dmoves);
+        t->xin = nullptr;
+        t->xout = nullptr;
+        nw_table_destroy(t);
+        return r;
+    };
+    auto hipchk = [&](hipError_t e, const char* what) {
+        return e == hipSuccess ? NW_OK : nwi::fail(NW_ERR_HIP, std::string("nw_first_path_banded: ") + what + ": " +
+                                                                   hipGetErrorString(e));
+    };
+    if ((rc = hipchk(hipMalloc(&rows, (size_t)std::max<int64_t>(K - 1, 1) * (size_t)L1 * 8), "hipMalloc(rows)")))
+        return done(rc == NW_ERR_HIP ? NW_ERR_OOM : rc);
+    if ((rc = hipchk(hipMalloc(&ctl, 64), "hipMalloc")) || (rc = hipchk(hipMalloc(&dmoves, (size_t)(L1 + band_rows)), "hipMalloc")))
+        return done(rc);
+    t->L2_total = L2;
+    t->epoch = 1;            // one producer per boundary, bands run one after the other
+    t->xblk = 1;
+    auto setup = [&](int64_t b, int64_t cols) -> int {
+        const int64_t r0 = b * band_rows, nr = std::min(band_rows, L2 - r0);
+        t->row_base = r0;
+        t->xin = b > 0 ? rows + (b - 1) * L1 : nullptr;
+        t->xout = nullptr;
+        return nw_table_set_sequences(t, s1, cols, s2 + r0, nr);
+    };
+    // 1. forward, score-only: bands 0 .. K-2 hand their bottom rows down
+    for (int64_t b = 0; b + 1 < K; ++b) {
+        if ((rc = setup(b, L1))) return done(rc);
+        t->xout = rows + b * L1;
+        if ((rc = nw_table_fill(t, m, k, d, 0u))) return done(rc);
+    }
+    // 2. backward: refill each band with codes, walk it bottom-up
+    int64_t ie = L1;
+    for (int64_t b = K - 1; b >= 0; --b) {
+        const int64_t r0 = b * band_rows, nr = std::min(band_rows, L2 - r0);
+        if (ie == 0) {       // on column 0: up moves to (0, 0)
+            path.insert(path.end(), (size_t)nr, (uint8_t)2);
+            continue;
+        }
+        if ((rc = setup(b, ie))) return done(rc);
+        if ((rc = nw_table_fill(t, m, k, d, NW_OUT_DIRS))) return done(rc);
+        if ((rc = hipchk(hipMemsetAsync(ctl, 0, 64, t->stream), "hipMemset"))) return done(rc);
+        nw_first_path_kernel<<<1, 64, 0, t->stream>>>(t->D, t->lay_NC, t->skew, (int32_t)ie, (int32_t)nr, b == 0 ? 1 : 0,
+                                                      dmoves, ctl);
+        if ((rc = hipchk(hipGetLastError(), "first path kernel"))) return done(rc);
+        uint32_t hc[8];
+        if ((rc = hipchk(hipMemcpyAsync(hc, ctl, sizeof hc, hipMemcpyDeviceToHost, t->stream), "hipMemcpy")))
+            return done(rc);
+        if ((rc = hipchk(hipStreamSynchronize(t->stream), "hipStreamSynchronize"))) return done(rc);
+        if (hc[4]) return done(nwi::fail(NW_ERR_STATE, "nw_first_path_banded: a cell on the path has no direction code"));
+        const size_t off = path.size();
+        path.resize(off + hc[3]);
+        if (hc[3] > 0 &&
+            (rc = hipchk(hipMemcpy(path.data() + off, dmoves, hc[3], hipMemcpyDeviceToHost), "hipMemcpy(moves)")))
+            return done(rc);
+        ie = hc[5];
+    }
+    if ((int64_t)path.size() > L1 + L2) return done(nwi::fail(NW_ERR_HIP, "nw_first_path_banded: path too long"));
+    std::reverse_copy(path.begin(), path.end(), moves);
+    *n = (int64_t)path.size();
+    return done(NW_OK);
 }
 
 }  // extern "C"

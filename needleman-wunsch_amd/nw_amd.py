@@ -57,6 +57,7 @@ EXPORTS = (
     "nw_table_stats", "nw_table_elapsed_ms", "nw_table_hash", "nw_table_copy_scores",
     "nw_table_copy_codes", "nw_table_copy_last_column", "nw_table_score_pitch", "nw_table_waves",
     "nw_table_trace", "nw_table_count_alignments", "nw_table_first_path", "nw_table_walk_elapsed_ms",
+    "nw_first_path_banded",
     # include/nw_panel.h
     "nw_panel_partition", "nw_panel_chain", "nw_panel_get_id", "nw_panel_create", "nw_panel_ipc_handle",
     "nw_panel_ipc_connect", "nw_panel_group_create", "nw_panel_destroy", "nw_panel_set_sequences",
@@ -150,6 +151,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "nw_table_count_alignments": (c_int, [c_p, P(c_u32)]),
         "nw_table_first_path": (c_int, [c_p, c_p, c_i64, P(c_i64)]),
         "nw_table_walk_elapsed_ms": (c_int, [c_p, P(ctypes.c_float), P(ctypes.c_float)]),
+        "nw_first_path_banded": (c_int, [c_int, ctypes.c_char_p, c_i64, ctypes.c_char_p, c_i64, c_i32, c_i32, c_i32,
+                                         c_i64, c_p, c_i64, P(c_i64)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -484,6 +487,20 @@ def walk(s1, s2, m: int, k: int, d: int, device: int = -1):
 
 
 # ----------------------------------------------------------------- inputs
+def first_path_banded(s1, s2, m: int, k: int, d: int, band_rows: int = 65536, device: int = -1) -> np.ndarray:
+    """Moves of the reference's first printed alignment (1 diag, 2 up, 4 left,
+    forward order) without the full table: nw_first_path_banded (checkpointed
+    bands of `band_rows` rows, a multiple of 64)."""
+    lib = load()
+    b1, b2 = _bytes(s1), _bytes(s2)
+    cap = len(b1) + len(b2)
+    out = np.zeros(max(cap, 1), dtype=np.uint8)
+    n = ctypes.c_int64()
+    _check(lib.nw_first_path_banded(device, b1, len(b1), b2, len(b2), m, k, d, band_rows, out.ctypes.data, cap,
+                                    ctypes.byref(n)), "nw_first_path_banded")
+    return out[:n.value]
+
+
 def gen_dna(seed: int, n: int) -> bytes:
     """splitmix64 i.i.d. DNA: base = "ACGT"[z >> 62]."""
     if n == 0:

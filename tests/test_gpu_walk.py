@@ -145,3 +145,48 @@ def test_walk_100k():
     assert len(mv) == case["path_len"]
     assert "%016x" % nw_amd.fnv1a64(mv.tobytes()) == case["path_fnv"]
     assert count == case["count"]
+
+
+@pytest.mark.parametrize("L1,L2,mkd,band", [
+    (3000, 1000, (2, 3, 5), 64), (1000, 3000, (1, 1, 1), 128), (513, 1025, (1, 1, 1), 192),
+    (4097, 333, (3, 2, 1), 64), (2048, 2048, (1, 1, -1), 1024), (1000, 3000, (0, 0, 0), 256),
+    (200, 1, (1, 1, 1), 64), (1, 200, (1, 1, 1), 64), (300, 640, (5, -4, 2), 64), (700, 500, (1, 1, 1), 4096),
+])
+def test_banded_first_path_vs_oracle(L1, L2, mkd, band):
+    """nw_first_path_banded (checkpointed bands, no full table) == the
+    reference's first printed alignment (oracle greedy walk)."""
+    s1, s2 = O.gen_dna(5, L1), O.gen_dna(6, L2)
+    mv = nw_amd.first_path_banded(s1, s2, *mkd, band_rows=band)
+    _, D, _ = O.fill(s1, s2, *mkd)
+    want = O.first_path(D)
+    assert len(mv) == len(want) and np.array_equal(mv, want)
+
+
+def test_banded_first_path_ties_bytes_and_edges():
+    s1, s2 = b"A" * 700, b"A" * 900            # every cell ties
+    _, D, _ = O.fill(s1, s2, 0, 0, 0)
+    assert np.array_equal(nw_amd.first_path_banded(s1, s2, 0, 0, 0, band_rows=64), O.first_path(D))
+    rng = np.random.default_rng(11)
+    s1 = bytes(rng.integers(33, 127, 777, dtype=np.uint8))
+    s2 = bytes(rng.integers(33, 127, 555, dtype=np.uint8))
+    _, D, _ = O.fill(s1, s2, 3, 2, 1)
+    assert np.array_equal(nw_amd.first_path_banded(s1, s2, 3, 2, 1, band_rows=128), O.first_path(D))
+    for a, b in [(b"", b"ACGT"), (b"ACGT", b""), (b"", b"")]:
+        assert nw_amd.first_path_banded(a, b, 1, 1, 1, band_rows=64).tolist() == [2] * len(b) + [4] * len(a)
+    with pytest.raises(nw_amd.NWError) as e:
+        nw_amd.first_path_banded(b"ACGT", b"ACGT", 1, 1, 1, band_rows=100)
+    assert e.value.rc == nw_amd.NW_ERR_ARG
+
+
+def test_banded_first_path_100k():
+    """100k x 100k through 13 bands of 8192 rows (0.4 GB of codes instead of
+    5 GB): the restatement's first-path fixture."""
+    path = os.path.join(os.path.dirname(__file__), "golden", "big_walk.json")
+    case = json.load(open(path))[0]
+    L1, L2, m, k, d = case["L1"], case["L2"], case["m"], case["k"], case["d"]
+    s1, s2 = nw_amd.gen_dna(1, L1), nw_amd.gen_dna(2, L2)
+    mv = nw_amd.first_path_banded(s1, s2, m, k, d, band_rows=8192)
+    sc, i, j = _path_score(s1, s2, mv, m, k, d)
+    assert (i, j) == (L1, L2) and sc == case["corner"]
+    assert len(mv) == case["path_len"]
+    assert "%016x" % nw_amd.fnv1a64(mv.tobytes()) == case["path_fnv"]
