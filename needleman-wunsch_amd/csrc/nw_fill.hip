@@ -566,7 +566,8 @@ struct TableView {
     int64_t spitch;
     const uint32_t* D;      // codes, or null
     int32_t NC;             // chunks per stripe of the layout (scan: ceil(L1/8); skew: ceil((L1+63)/8))
-    int32_t skew;           // 1: skewed layout (nw_skew.inc), 0: column layout (scan kernel)
+    int32_t skew;           // 1: skewed layout (nw_skew.hip), 0: column layout (scan kernel)
+    int32_t pair;           // 1: column layout with rows permuted (nw_pair.hip)
     int32_t d;
     int32_t row_base;       // panels: global row of local row 0
     const uint64_t* top;    // panels: boundary row granules (H - d), or null for row 0 = seed
@@ -582,7 +583,11 @@ struct TableView {
 // Column tiles: g*spitch + (i-1)*64 + l, one 256-byte store per column.
 // Skewed layout (nw_skew.inc): stored by step t = c + (r & 63) instead of
 // by column, same quad tiles.
-__host__ __device__ __forceinline__ int64_t score_index(int64_t r, int64_t c, int64_t spitch, bool skew = false) {
+// Pair layout (nw_pair.hip): the column layout of the permuted row
+// nwi::pair_row(r).
+__host__ __device__ __forceinline__ int64_t score_index(int64_t r, int64_t c, int64_t spitch, bool skew = false,
+                                                         bool pair = false) {
+    if (pair) r = nwi::pair_row(r);
     if (skew) c += r & 63;
 #if NW_SCORE_X4
     return (r >> 6) * spitch + ((c >> 2) * 64 + (r & 63)) * 4 + (c & 3);
@@ -592,8 +597,10 @@ __host__ __device__ __forceinline__ int64_t score_index(int64_t r, int64_t c, in
 }
 
 // Code word and bit position of interior cell (i, j) (see include/nw_fill.h).
-__host__ __device__ __forceinline__ int64_t code_word(int64_t i, int64_t j, int64_t NC, bool skew, int* shift) {
-    const int64_t g = (j - 1) >> 6, l = (j - 1) & 63;
+__host__ __device__ __forceinline__ int64_t code_word(int64_t i, int64_t j, int64_t NC, bool skew, int* shift,
+                                                      bool pair = false) {
+    const int64_t rr = pair ? nwi::pair_row(j - 1) : j - 1;
+    const int64_t g = rr >> 6, l = rr & 63;
     const int64_t t = (i - 1) + (skew ? l : 0);
     *shift = 21 - 3 * (int)(t & 7);
     return (g * (NC + 1) + (t >> 3) + 1) * 64 + l;
@@ -602,7 +609,7 @@ __host__ __device__ __forceinline__ int64_t code_word(int64_t i, int64_t j, int6
 __device__ __forceinline__ int32_t score_at(const TableView& v, int64_t i, int64_t j) {
     if (i == 0) return (int32_t)(-(j + v.row_base) * (int64_t)v.d);
     if (j == 0) return v.top ? (int32_t)(uint32_t)v.top[i - 1] + v.d : (int32_t)(-i * (int64_t)v.d);
-    return v.tiles[score_index(j - 1, i - 1, v.spitch, v.skew)];
+    return v.tiles[score_index(j - 1, i - 1, v.spitch, v.skew, v.pair)];
 }
 
 // Dense i-major copy of columns [i0, i1): out[(i-i0)*(L2+1) + j].
@@ -621,7 +628,7 @@ __device__ __forceinline__ uint32_t code_at(const TableView& v, int64_t i, int64
     if (i == 0) return j == 0 ? 0u : 2u;          // (0,0): none; (0,j): up
     if (j == 0) return 4u;                         // (i,0): left
     int sh;
-    const int64_t wd = code_word(i, j, v.NC, v.skew, &sh);
+    const int64_t wd = code_word(i, j, v.NC, v.skew, &sh, v.pair);
     return (v.D[wd] >> sh) & 7u;
 }
 
@@ -733,6 +740,7 @@ TableView view_of(const nw_table* t) {
     v.D = (t->last_mask & NW_OUT_DIRS) ? t->D : nullptr;
     v.NC = (int32_t)t->lay_NC;
     v.skew = t->skew;
+    v.pair = t->pair;
     v.d = t->last_d;
     v.row_base = (int32_t)t->row_base;
     v.top = t->row_base > 0 ? t->xin : nullptr;
@@ -774,9 +782,9 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
     NW_HIPCHK(hipEventRecord(t->ev[0], t->stream));
     NW_HIPCHK(hipMemsetAsync(t->ctl, 0, CTL_WORDS * 4, t->stream));
     int W = 0;
-    bool skew = false;
+    bool skew = false, pair = false;
     if (L1 > 0 && L2 > 0) {
-        const StripePlan plan = plan_stripes(t->NG, t->ncu);
+        StripePlan plan = plan_stripes(t->NG, t->ncu);
         W = plan.W;
         // Profile lookups when the sequences were coded to <= 8 symbols and
         // sub' fits a signed byte ($NW_PROF=0 forces the byte compares).
@@ -795,11 +803,20 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         const char* ke = getenv("NW_KERNEL");
         if (ke && std::strcmp(ke, "skew") == 0) skew = true;
         else if (ke && std::strcmp(ke, "scan") == 0) skew = false;
+        else if (ke && std::strcmp(ke, "pair") == 0) pair = true;
         else skew = t->NG <= 4 * (int64_t)t->ncu && L1 >= 4 * L2;
-        KernelFn fn = skew ? pick_skew(W, prof, sh, sd, stt) : pick_kernel(W, prof, sh, sd, stt);
+        // a feeding panel's last row must be lane 63's row b of its last pair stripe
+        if (pair && t->xout && L2 % 128 != 0) pair = false;
+        const int64_t NGk = pair ? (L2 + 127) / 128 : t->NG;
+        if (pair) {
+            plan = plan_stripes(NGk, t->ncu);
+            W = plan.W;
+        }
+        KernelFn fn = skew ? pick_skew(W, prof, sh, sd, stt)
+                           : pair ? pick_pair(W, prof, sh, sd, stt) : pick_kernel(W, prof, sh, sd, stt);
         if (!fn) return fail(NW_ERR_ARG, "nw_table_fill: unsupported wave count");
         const int64_t NCH = skew ? (L1 + 63 + CH - 1) / CH : t->NC;
-        t->spitch = 512 * NCH;
+        t->spitch = 512 * NCH;          // per 64-row stripe (a pair stripe is two of them)
         FillArgs a{};
         a.s1 = t->s1;
         a.s2 = t->s2;
@@ -810,12 +827,12 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         a.d = d;
         a.NC = (int32_t)t->NC;
         a.NCH = (int32_t)NCH;
-        a.NG = (int32_t)t->NG;
+        a.NG = (int32_t)NGk;
         a.NSW = (int32_t)plan.NSW;
         a.SQ = plan.SQ;
         a.SR = plan.SR;
         a.H = t->H;
-        a.spitch = t->spitch;
+        a.spitch = pair ? 2 * t->spitch : t->spitch;
         a.D = t->D;
         a.lastcol = t->lastcol;
         a.gran = t->gran;
@@ -875,6 +892,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
     t->pend_d = d;
     t->pend_W = W;
     t->pend_skew = skew;
+    t->pend_pair = pair;
     return NW_OK;
 }
 
@@ -898,7 +916,7 @@ int fill_finish(nw_table* t) {
     int32_t corner = 0;
     if (L1 > 0 && L2 > 0) {
         const int64_t r = L2 - 1, q = L1 - 1;
-        const int32_t* src = sh ? t->H + score_index(r, q, t->spitch, t->pend_skew) : t->lastcol + L2;
+        const int32_t* src = sh ? t->H + score_index(r, q, t->spitch, t->pend_skew, t->pend_pair) : t->lastcol + L2;
         NW_HIPCHK(hipMemcpyAsync(&corner, src, 4, hipMemcpyDeviceToHost, t->stream));
     }
     NW_HIPCHK(hipStreamSynchronize(t->stream));
@@ -917,6 +935,7 @@ int fill_finish(nw_table* t) {
     t->last_d = d;
     t->waves = t->pend_W;
     t->skew = t->pend_skew;
+    t->pair = t->pend_pair;
     t->lay_NC = t->spitch / 512;
     return NW_OK;
 }
@@ -1009,11 +1028,11 @@ int nw_table_create(int device, int64_t max_L1, int64_t max_L2, uint32_t out_mas
     if ((rc = alloc((void**)&t->s1, (size_t)(CH * NC + 64)))) return bail(rc);
     if ((rc = alloc((void**)&t->s2, (size_t)(64 * NG + 1024)))) return bail(rc);
     if (out_mask & NW_OUT_SCORES) {
-        if ((rc = alloc((void**)&t->H, (size_t)std::max<int64_t>(NG, 1) * (size_t)(NC + 8) * 2048)))
+        if ((rc = alloc((void**)&t->H, (size_t)(NG + 1) * (size_t)(NC + 8) * 2048)))
             return bail(rc);
     }
     if (out_mask & NW_OUT_DIRS) {
-        if ((rc = alloc((void**)&t->D, (size_t)std::max<int64_t>(NG, 1) * (NC + 9) * 256))) return bail(rc);
+        if ((rc = alloc((void**)&t->D, (size_t)(NG + 1) * (NC + 9) * 256))) return bail(rc);
     }
     if ((rc = alloc((void**)&t->lastcol, (size_t)(64 * NG + 128) * 4))) return bail(rc);
     // Granule slots: one per concurrently running WG-stripe + 1.

@@ -20,7 +20,8 @@ struct nw_table {
     // geometry for the current sequences
     int64_t L1 = -1, L2 = -1;
     int64_t NC = 0, NG = 0, spitch = 0;   // NC = ceil(L1/8) column chunks; spitch: see fill_launch
-    int skew = 0;                   // layout of the tables: 1 = skewed (nw_skew.inc), 0 = column (scan)
+    int skew = 0;                   // layout of the tables: 1 = skewed (nw_skew.hip), 0 = column (scan)
+    int pair = 0;                   // 1: column layout with rows permuted (nw_pair.hip, nwi::pair_row)
     int64_t lay_NC = 0;             // chunks per stripe of that layout
     int alpha = 0;                  // s1/s2 coded to symbols 0..alpha-1 on the device (<= 8), 0: raw bytes
     // device buffers
@@ -48,6 +49,7 @@ struct nw_table {
     int32_t pend_d = 0;
     int pend_W = 0;
     int pend_skew = 0;
+    int pend_pair = 0;
     // results of the last fill
     bool filled = false;
     uint32_t last_mask = 0;
@@ -76,6 +78,13 @@ int poison(uint64_t* p, int64_t n, uint32_t epoch, hipStream_t s);
 void walk_release(nw_table* t);
 
 constexpr int kChunk = 8;   // columns per chunk (hand-off granules per chunk)
+
+// The pair kernel's row permutation: row r (0-based) of the table lives at
+// row pair_row(r) of the 64-row column layout (lane (r%128)/2 of virtual
+// stripe 2*(r/128) + r%2).
+__host__ __device__ __forceinline__ int64_t pair_row(int64_t r) {
+    return 64 * (2 * (r >> 7) + (r & 1)) + ((r & 127) >> 1);
+}
 
 }  // namespace nwi
 

@@ -94,10 +94,18 @@ __device__ __forceinline__ void lds_publish(int* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// Compiler-only fence for the LDS ring handshakes written in C++: the LDS
+// performs one wave's DS instructions in issue order, so keeping the plain
+// slot reads / writes on their side of the relaxed counter accesses in the
+// instruction stream is all the ordering they need.
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
 using KernelFn = void (*)(FillArgs);
 
 // nw_skew.hip: the skewed-stripe kernel for W compute waves per workgroup
 // (nullptr for an unsupported W).
 KernelFn pick_skew(int W, bool prof, bool sh, bool sd, bool stt);
+// nw_pair.hip: the two-rows-per-lane scan kernel.
+KernelFn pick_pair(int W, bool prof, bool sh, bool sd, bool stt);
 
 }  // namespace nwk

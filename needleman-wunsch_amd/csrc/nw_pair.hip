@@ -1,0 +1,374 @@
+// nw_pair.hip -- the two-rows-per-lane column-scan fill kernel (the "pair"
+// kernel; launched by nwi::fill_launch in nw_fill.hip, which also holds the
+// one-row scan kernel; shared definitions in nw_kern.h).
+//
+// Same hot path -- compute_table_scores() (needleman-wunsch.c:583-626 ->
+// score_cell :418-510) -- and the same stripe scan as nw_fill_kernel, but a
+// wave owns a 128-row stripe: lane l holds rows a = j0 + 2l and b = a + 1.
+// At 100k rows that is 782 waves instead of 1563, so every SIMD runs at most
+// one compute wave (the one-row kernel doubles up on half of them and the
+// whole stripe chain moves at the two-wave rate).  One column step:
+//
+//   Xa  = max3(Ga, sh + sub'_a, T)          left, diag (lane l-1's row b), row above
+//   Xb  = max3(Gb, Ga + sub'_b, Xa)          left, diag (own row a), up (own row a)
+//   Gb' = prefix max of Xb over the lanes    the 6-level DPP scan of the one-row kernel
+//   sh' = wave_shr1(Gb'), lane 0 <- T        row b of lane l-1 = the cell above row a
+//   Ga' = max(Xa, sh')
+//
+// in the one-row kernel's domain G' = H + r*d + (i - base)*d (r = row offset
+// inside the workgroup, i = column), where left and up cost nothing and
+// diag = G'(i-1, r-1) + sub', sub' = m + 2d | 2d - k (needleman-wunsch.c:
+// 429-465).  Including the row above T in every lane's Xa is harmless: G' is
+// non-decreasing down a column.  Direction flags: needleman-wunsch.c:485-503.
+//
+// Layout (nw_table.pair = 1): the one-row kernel's layout with rows
+// permuted -- row r of the table is row rperm(r) = 64*(2*(r/128) + r%2) +
+// (r%128)/2 of a 64-row layout ("virtual stripes" 2g and 2g+1 hold the a and
+// b rows of pair stripe g), so every reader only maps the row.
+
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+#include <type_traits>
+
+#include "nw_kern.h"
+
+namespace nwk {
+namespace {
+
+// Count 3-bit codes of a word (8 per word, bits 0..23) with >= 2 directions.
+__device__ __forceinline__ uint32_t branch_codes(uint32_t x) {
+    const uint32_t y = (x & (x >> 1)) | (x & (x >> 2)) | ((x >> 1) & (x >> 2));
+    return __builtin_popcount(y & 0x249249u);
+}
+
+// wave_shr:1, lane 0 <- old.
+__device__ __forceinline__ int shr1(int old, int v) { return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xf, 0xf, false); }
+
+// Inclusive prefix max over the 64 lanes (row_shr 1/2/4/8, row_bcast 15/31).
+__device__ __forceinline__ int prefmax(int x) {
+    x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0x111, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0x112, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0x114, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0x118, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0x142, 0xa, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0x143, 0xc, 0xf, false));
+    return x;
+}
+
+__device__ __forceinline__ void pair_store_scores(const int* h, int32_t* p) {
+    typedef int v4i_ __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(v4i_{h[0], h[1], h[2], h[3]}, reinterpret_cast<v4i_*>(p));
+    __builtin_nontemporal_store(v4i_{h[4], h[5], h[6], h[7]}, reinterpret_cast<v4i_*>(p + 256));
+}
+
+template <int W, bool SH, bool SD, bool ST, bool PROF>
+__global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
+    constexpr int R = 4;
+    constexpr int NOCONS = 1 << 30;
+    __shared__ __attribute__((aligned(16))) int tring[(W + 1) * R * SLOT];
+    __shared__ __attribute__((aligned(8))) int ctr[2 * W + 4];
+    __shared__ int sh_sidx;
+    __shared__ int sh_abort;
+
+    const int lane = threadIdx.x & 63;
+    const int w = uni(threadIdx.x >> 6);
+    const bool loader = (w == W);
+    const int d = a.d;
+    const int vcm = a.m + 2 * a.d;
+    const int vck = 2 * a.d - a.k;
+    const int NC = a.NC;
+    const int nlast = a.L1 - CH * (NC - 1);   // columns in the last chunk (1..8)
+
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const int sidx = (int)atomicAdd(&a.ctl[CTL_NEXT], 1u);
+            sh_sidx = sidx;
+            sh_abort = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - (sidx * a.SQ + min(sidx, a.SR)));
+            for (int v = 0; v <= W; ++v) {
+                ctr[2 * v + 2] = 0;
+                ctr[2 * v + 1] = v < nw ? 0 : NOCONS;
+            }
+        }
+        __syncthreads();
+        const int sidx = uni(sh_sidx);
+        if (sidx >= a.NSW || sh_abort) break;
+        if (a.trace && threadIdx.x == 0) {
+            a.trace[8 * (int64_t)sidx + 0] = __builtin_amdgcn_s_memrealtime();
+            a.trace[8 * (int64_t)sidx + 3] = (uint64_t)blockIdx.x | ((uint64_t)__smid() << 32);
+        }
+        const int g0 = sidx * a.SQ + min(sidx, a.SR);                 // first pair stripe of the WG-stripe
+        const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - g0);
+        const int g = g0 + w;
+        const bool real = !loader && w < nw;
+        const int j0 = 1 + 128 * g;                // first row of the pair stripe
+        const int ja = j0 + 2 * lane, jb = ja + 1; // this lane's rows
+        int gav = 0;
+        uint32_t bc = 0;
+
+        if (loader) {
+            // ---------------- loader wave: ring 0 (as the one-row kernel's) ----------------
+            const bool seeded = sidx == 0 && !a.xin;
+            const bool xsrc = sidx == 0 && a.xin;
+            const uint64_t* gin = xsrc ? a.xin : a.gran + (int64_t)(sidx % a.nslot) * a.gpitch;
+            const uint32_t want = xsrc ? a.epoch : (uint32_t)sidx;
+            const uint32_t* s1w = reinterpret_cast<const uint32_t*>(a.s1);
+            const bool chl = lane == 8 || lane == 9;
+            const int wk = lane >> 3, wb = lane & 7;
+            const int64_t ngr = (int64_t)CH * NC;
+            auto gload = [&](int cf) -> uint64_t {
+                const int64_t x = (int64_t)CH * cf + lane;
+                return x < ngr ? ld_gran(gin + x, xsrc) : 0ull;
+            };
+            int cw = 0;
+            uint64_t pf = 0, pn = 0;
+            uint32_t pc = chl ? s1w[lane - 8] : 0u;
+            if (!seeded) {
+                pf = gload(0);
+                pn = gload(CH);
+            }
+            for (int c = 0; c < NC; ++c) {
+                const int n = (c == NC - 1) ? nlast : CH;
+                if (c == cw + CH) {
+                    cw += CH;
+                    pf = pn;
+                    if (!seeded) pn = gload(cw + CH);
+                }
+                while (lds_ld(&ctr[1]) < c - R + 1) __builtin_amdgcn_s_sleep(1);
+                int* dst = &tring[(c % R) * SLOT];
+                const int base = chunk_base(c);
+                if (seeded) {
+                    // row 0: H[i][0] - d = -(i+1)*d (computation.c:102-110) -> G' = -(base+1)*d
+                    if (lane < CH) dst[lane] = -(base + 1) * d;
+                } else {
+                    const bool mine = wk == c - cw;
+                    bool ok = !mine || wb >= n || (uint32_t)(pf >> 32) == want;
+                    if (!__all(ok)) {
+                        const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+                        for (;;) {
+                            __builtin_amdgcn_s_sleep(1);
+                            if (wk >= c - cw && (uint32_t)(pf >> 32) != want) pf = gload(cw);
+                            ok = !mine || wb >= n || (uint32_t)(pf >> 32) == want;
+                            if (__all(ok)) break;
+                            const int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
+                            const uint32_t ab = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT);
+                            const bool peer = xsrc && __any(mine && wb < n && (uint32_t)(pf >> 32) == (want | POISON_BIT));
+                            if (ab || peer || now - t0 > a.spin_ticks) {
+                                if (lane == 0) {
+                                    __hip_atomic_store(&a.ctl[CTL_ABORT], 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                                    if (!ab)
+                                        atomicCAS(&a.ctl[CTL_ERR], 0u,
+                                                  (uint32_t)(peer ? NW_ERR_PEER : NW_ERR_TIMEOUT));
+                                    __hip_atomic_store(&sh_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                }
+                                break;
+                            }
+                        }
+                    }
+                    if (lds_ld(&sh_abort)) break;
+                    // H - d of the row above -> G' of row -1: + (i - base)*d
+                    if (mine) dst[wb] = (int)(uint32_t)pf + (CH * c + wb + 1 - base) * d;
+                }
+                if (chl) {
+                    dst[lane] = (int)pc;
+                    if (c + 1 < NC) pc = s1w[2 * (c + 1) + lane - 8];
+                }
+                lds_order();
+                if (lane == 0) lds_publish(&ctr[2], c + 1);
+            }
+        } else if (real) {
+            // ---------------- compute wave: its 128-row stripe, chunk by chunk ----
+            uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
+            // virtual 64-row stripes 2g (rows a) and 2g+1 (rows b): a.spitch = 1024*NC
+            int32_t* tileA = a.H + (int64_t)g * a.spitch;
+            int32_t* tileB = tileA + a.spitch / 2;
+            uint32_t* dtileA = a.D + (int64_t)(2 * g) * (NC + 1) * 64;
+            uint32_t* dtileB = dtileA + (int64_t)(NC + 1) * 64;
+            const bool publish = (w == nw - 1) && sidx + 1 < a.NSW;
+            // the panel's last row is row b of lane 63 (feeding panels have 128*k rows)
+            const bool xpublish = a.xout && g == a.NG - 1;
+            const bool okA = ja <= a.L2, okB = jb <= a.L2;
+            const int* tin = &tring[w * R * SLOT];
+            int* tout = &tring[(w + 1) * R * SLOT];
+            const int* cin = &ctr[2 * w + 1];          // {cons[w], prog[w], cons[w+1]}
+            const uint32_t c2a = a.s2[ja - 1], c2b = a.s2[jb - 1];
+            // column 0 (and the row above at column 0): G' = -(1 + row_base + 128*g0)*d
+            const int C0 = -(1 + a.row_base + 128 * g0) * d;
+            int Ga = C0, Gb = C0, sh = C0;
+            int nloa = -(128 * w + 2 * lane) * d;      // H = G' + nlo - (s+1)d in chunk 0
+            uint32_t accpA = 0, accpB = 0;
+            bool aborted = false;
+            if (a.trace && lane == 0 && w == 0) {
+                a.trace[8 * (int64_t)sidx + 1] = __builtin_amdgcn_s_memrealtime();
+                a.trace[8 * (int64_t)sidx + 4] = __builtin_amdgcn_s_memtime();
+            }
+            if (a.trace && lane == 0 && w == nw - 1) a.trace[8 * (int64_t)sidx + 6] = __builtin_amdgcn_s_memrealtime();
+            for (int c = 0; c < NC && !aborted; ++c) {
+                if (c > 0 && c % SUPER_CHUNKS == 0) {
+                    const int shv = SUPER_CHUNKS * CH * d;
+                    Ga -= shv;
+                    Gb -= shv;
+                    sh -= shv;
+                    nloa += shv;
+                }
+                const int n = (c == NC - 1) ? nlast : CH;
+                for (;;) {
+                    const int pin = uni(lds_ld(&cin[1]));
+                    const int pout = uni(lds_ld(&cin[2]));
+                    if (pin > c && pout >= c - R + 1) break;
+                    if (uni(lds_ld(&sh_abort))) {
+                        aborted = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (aborted) break;
+                lds_order();
+                const int* slot = &tin[(c % R) * SLOT];
+                int T[CH];
+#pragma unroll
+                for (int s = 0; s < CH; ++s) T[s] = slot[s];
+                const uint64_t sym8 = (uint64_t)(uint32_t)slot[8] | ((uint64_t)(uint32_t)slot[9] << 32);
+                lds_order();
+                if (lane == 0) lds_publish(&ctr[2 * w + 1], c + 1);
+                int* so = &tout[(c % R) * SLOT];
+                int ha[CH], hb[CH];
+                uint32_t accA = 0, accB = 0;
+#pragma unroll
+                for (int s = 0; s < CH; ++s) {
+                    if (s < n) {
+                        const uint32_t sym = (uint32_t)(sym8 >> (8 * s)) & 0xffu;
+                        const int dga = sh + (sym == c2a ? vcm : vck);
+                        const int Xa = max(max(Ga, dga), T[s]);
+                        const int dgb = Ga + (sym == c2b ? vcm : vck);
+                        const int Xb = max(max(Gb, dgb), Xa);
+                        const int Gbn = prefmax(Xb);
+                        const int shn = shr1(T[s], Gbn);
+                        const int Gan = max(Xa, shn);
+                        const uint32_t ca = (dga == Gan ? 1u : 0u) | (shn == Gan ? 2u : 0u) | (Ga == Gan ? 4u : 0u);
+                        const uint32_t cb = (dgb == Gbn ? 1u : 0u) | (Gan == Gbn ? 2u : 0u) | (Gb == Gbn ? 4u : 0u);
+                        accA = (accA << 3) | ca;
+                        accB = (accB << 3) | cb;
+                        ha[s] = Gan + nloa - (s + 1) * d;
+                        hb[s] = Gbn + nloa - (s + 2) * d;
+                        if (ST) {
+                            if (okA) gav = max(gav, ha[s] < 0 ? -ha[s] : ha[s]);
+                            if (okB) gav = max(gav, hb[s] < 0 ? -hb[s] : hb[s]);
+                        }
+                        if (lane == 63) so[s] = Gbn;
+                        Ga = Gan;
+                        Gb = Gbn;
+                        sh = shn;
+                    } else {
+                        ha[s] = hb[s] = 0;
+                    }
+                }
+                if (lane == 63) {                      // the chunk's symbols go down the ring (from
+                    so[8] = (int)(uint32_t)sym8;       // registers: the input slot was released above)
+                    so[9] = (int)(uint32_t)(sym8 >> 32);
+                }
+                if (n < CH) {
+                    accA <<= 3 * (CH - n);
+                    accB <<= 3 * (CH - n);
+                }
+                if (SH) {
+                    pair_store_scores(ha, tileA + (int64_t)c * 512 + lane * 4);
+                    pair_store_scores(hb, tileB + (int64_t)c * 512 + lane * 4);
+                }
+                if (SD) {
+                    __builtin_nontemporal_store(accA, dtileA + (int64_t)(c + 1) * 64 + lane);
+                    __builtin_nontemporal_store(accB, dtileB + (int64_t)(c + 1) * 64 + lane);
+                }
+                if (ST) {
+                    bc += branch_codes(okA ? accA : 0u);
+                    bc += branch_codes(okB ? accB : 0u);
+                }
+                if (!SH && c == NC - 1) {              // score-only: H[L1][*]
+                    a.lastcol[ja] = ha[n - 1];
+                    a.lastcol[jb] = hb[n - 1];
+                }
+                // (plain domain: H - d = G' - 128(w+1)d - (i - base)d)
+                if (publish || xpublish) {
+                    if (lane < n) {
+                        const int v = so[lane] - 128 * (w + 1) * d - (CH * c + lane + 1 - chunk_base(c)) * d;
+                        const uint64_t tag = publish ? (uint32_t)(sidx + 1) : a.epoch;
+                        const uint64_t gr = (tag << 32) | (uint32_t)v;
+                        if (publish)
+                            __hip_atomic_store(gout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        else
+                            __hip_atomic_store(a.xout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                    if (xpublish && a.xflag && ((c + 1) % a.xblk == 0 || c == NC - 1)) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (lane == 0)
+                            __hip_atomic_store(&a.xflag[c / a.xblk], a.epoch, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                }
+                lds_order();
+                if (lane == 0) lds_publish(&ctr[2 * w + 4], c + 1);
+                nloa -= CH * d;
+            }
+            (void)accpA;
+            (void)accpB;
+        }
+        if (a.trace && !loader && w == nw - 1 && lane == 0) {
+            a.trace[8 * (int64_t)sidx + 2] = __builtin_amdgcn_s_memrealtime();
+            a.trace[8 * (int64_t)sidx + 5] = __builtin_amdgcn_s_memtime();
+        }
+        if (ST && real) {
+            int gv = gav;
+            uint32_t bv = bc;
+            for (int o = 32; o > 0; o >>= 1) {
+                gv = max(gv, __shfl_xor(gv, o));
+                bv += __shfl_xor(bv, o);
+            }
+            if (lane == 0) {
+                atomicMax(reinterpret_cast<int*>(&a.ctl[CTL_GAV]), gv);
+                atomicAdd(&a.ctl[CTL_BC], bv);
+            }
+        }
+        __syncthreads();
+        if (sh_abort) break;
+    }
+}
+
+template <int W, bool P>
+KernelFn pick_flags(bool sh, bool sd, bool stt) {
+    if (sh && sd) return stt ? nw_pair_kernel<W, true, true, true, P> : nw_pair_kernel<W, true, true, false, P>;
+    if (sh) return stt ? nw_pair_kernel<W, true, false, true, P> : nw_pair_kernel<W, true, false, false, P>;
+    if (sd) return stt ? nw_pair_kernel<W, false, true, true, P> : nw_pair_kernel<W, false, true, false, P>;
+    return stt ? nw_pair_kernel<W, false, false, true, P> : nw_pair_kernel<W, false, false, false, P>;
+}
+
+template <int W>
+KernelFn pick_prof(bool prof, bool sh, bool sd, bool stt) {
+    return prof ? pick_flags<W, true>(sh, sd, stt) : pick_flags<W, false>(sh, sd, stt);
+}
+
+}  // namespace
+
+KernelFn pick_pair(int W, bool prof, bool sh, bool sd, bool stt) {
+    switch (W) {
+        case 1: return pick_prof<1>(prof, sh, sd, stt);
+        case 2: return pick_prof<2>(prof, sh, sd, stt);
+        case 3: return pick_prof<3>(prof, sh, sd, stt);
+        case 4: return pick_prof<4>(prof, sh, sd, stt);
+        case 5: return pick_prof<5>(prof, sh, sd, stt);
+        case 6: return pick_prof<6>(prof, sh, sd, stt);
+        case 7: return pick_prof<7>(prof, sh, sd, stt);
+        case 8: return pick_prof<8>(prof, sh, sd, stt);
+        case 10: return pick_prof<10>(prof, sh, sd, stt);
+        case 12: return pick_prof<12>(prof, sh, sd, stt);
+        case 15: return pick_prof<15>(prof, sh, sd, stt);
+        default: return nullptr;
+    }
+}
+
+}  // namespace nwk

@@ -233,6 +233,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
                 // window: copy k holds column p + 1 + k at position p
                 swin[wk * SWN + ((CH * c + wb - wk) & (SWN - 1))] = pc;
                 pc = a.s1[CH * (c + 1) + wb];
+                lds_order();
                 if (lane == 0) lds_publish(&ctr[2], c + 9);   // prog = slots done + 8
             }
         } else if (real) {
@@ -335,16 +336,18 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
             // ---- generic chunk (prologue / epilogue, every lane checked) ----
             auto generic_chunk = [&](int c) -> bool {
                 const bool need_in = c < NC1;
-                for (int spins = 0;; ++spins) {
+                for (;;) {
                     const int pin = uni(lds_ld(&cin[1]));
                     const int pout = uni(lds_ld(&cin[2]));
                     if ((!need_in || pin > c + 8) && pout >= c - 6 - R) break;
                     if (uni(lds_ld(&sh_abort))) return false;
                     __builtin_amdgcn_s_sleep(1);
                 }
+                lds_order();
                 int T[CH];
 #pragma unroll
                 for (int s = 0; s < CH; ++s) T[s] = need_in ? tin[(c % R) * SLOT + s] : 0;
+                lds_order();
                 if (need_in && lane == 0) lds_publish(&ctr[2 * w + 1], c + 1);
                 const uint64_t wv = *reinterpret_cast<const uint64_t*>(&swin[0] + (waddr(c) - lds_addr(&swin[0])));
                 const int off = (CH * c + 1 - base) * d;     // E - H at step 8c
@@ -382,6 +385,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
                     for (int q = done; q < ndone; ++q) publish_slot(q);
                 if (ndone > done) {
                     done = ndone;
+                    lds_order();
                     if (lane == 0) lds_publish(&ctr[2 * w + 4], done + 8);
                 }
                 return true;
@@ -392,7 +396,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
             const int cmid = NC1 - 1;   // the chunk where lane 0 reaches column L1 stays generic (last column)
             SkewSlot tA, tB;
             auto wait_slot = [&](int c, SkewSlot& tt) -> bool {
-                for (int spins = 0;; ++spins) {
+                for (;;) {
                     const uint64_t pq = skew_read_slot(kc.cb, rd[c % R], waddr(c), tt);
                     const int pin = uni((int)(uint32_t)pq), pout = uni((int)(pq >> 32));
                     if (pin > c + 8 && pout >= c - 6 - R) return true;

@@ -50,6 +50,7 @@ struct CountArgs {
     const uint32_t* D;    // codes, include/nw_fill.h layout
     int64_t NC;           // 8-step chunks per stripe of the table's layout
     int32_t skew;         // skewed layout: lane l's word index runs ahead by l steps
+    int32_t pair;         // pair layout: rows permuted (nwi::pair_row)
     int32_t L1, L2, NG;
     uint64_t* rows;       // granule (g, i) at g*L1 + i-1: P(i, 64(g+1)) for stripe g < NG-1
     uint32_t* ctl;
@@ -76,7 +77,8 @@ __global__ __launch_bounds__(64) void nw_count_kernel(CountArgs a) {
         if (g >= a.NG) return;
         if (__hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
 
-        const uint32_t* Dg = a.D + ((int64_t)g * (a.NC + 1) + 1) * 64 + lane;
+        const int64_t rr = a.pair ? nwi::pair_row(64 * (int64_t)g + lane) : 64 * (int64_t)g + lane;
+        const uint32_t* Dg = a.D + ((rr >> 6) * (a.NC + 1) + 1) * 64 + (rr & 63);
         const uint64_t* top = g > 0 ? a.rows + (int64_t)(g - 1) * a.L1 : nullptr;
         uint64_t* bot = g < a.NG - 1 ? a.rows + (int64_t)g * a.L1 : nullptr;
         uint32_t P = 1;         // column 0: (0,j) has only the up code, P = 1
@@ -160,8 +162,9 @@ __global__ __launch_bounds__(64) void nw_count_kernel(CountArgs a) {
 // top = 1: row 0 is the seeded first row, so the walk runs on along row 0 /
 // column 0 to (0, 0); top = 0 (a band of rows below another): it stops on
 // row 0, which is the band above's last row.
-__global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, int64_t NC, int32_t skew, int32_t i0,
-                                                           int32_t j0, int32_t top, uint8_t* moves, uint32_t* ctl) {
+__global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, int64_t NC, int32_t skew, int32_t pair,
+                                                           int32_t i0, int32_t j0, int32_t top, uint8_t* moves,
+                                                           uint32_t* ctl) {
     __shared__ uint32_t blk[8][64];
     const int lane = threadIdx.x;
     int i = i0, j = j0;
@@ -174,9 +177,10 @@ __global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, in
         const int64_t q = t >> 3, q0 = q & ~(int64_t)7;
         if (g != gb || q0 != qb) {
             __syncthreads();
+            const int64_t rr = pair ? nwi::pair_row(64 * (int64_t)g + lane) : 64 * (int64_t)g + lane;
 #pragma unroll
             for (int x = 0; x < 8; ++x)
-                blk[x][lane] = q0 + x < NC ? D[((int64_t)g * (NC + 1) + q0 + x + 1) * 64 + lane] : 0u;
+                blk[x][lane] = q0 + x < NC ? D[((rr >> 6) * (NC + 1) + q0 + x + 1) * 64 + (rr & 63)] : 0u;
             __syncthreads();
             gb = g;
             qb = q0;
@@ -272,6 +276,7 @@ int nw_table_count_alignments(nw_table* t, uint32_t* count) {
     a.D = t->D;
     a.NC = t->lay_NC;
     a.skew = t->skew;
+    a.pair = t->pair;
     a.L1 = (int32_t)t->L1;
     a.L2 = (int32_t)t->L2;
     a.NG = (int32_t)NG;
@@ -311,8 +316,8 @@ int nw_table_first_path(nw_table* t, uint8_t* moves, int64_t cap, int64_t* n) {
     }
     NW_HIPCHK(hipMemsetAsync(w->ctl, 0, 64, t->stream));
     NW_HIPCHK(hipEventRecord(t->ev[2], t->stream));
-    nw_first_path_kernel<<<1, 64, 0, t->stream>>>(t->D, t->lay_NC, t->skew, (int32_t)t->L1, (int32_t)t->L2, 1, w->moves,
-                                                  w->ctl);
+    nw_first_path_kernel<<<1, 64, 0, t->stream>>>(t->D, t->lay_NC, t->skew, t->pair, (int32_t)t->L1, (int32_t)t->L2, 1,
+                                                  w->moves, w->ctl);
     NW_HIPCHK(hipGetLastError());
     NW_HIPCHK(hipEventRecord(t->ev[3], t->stream));
     uint32_t ctl[8];
@@ -422,8 +427,8 @@ int nw_first_path_banded(int device, const char* s1, int64_t L1, const char* s2,
         if ((rc = setup(b, ie))) return done(rc);
         if ((rc = nw_table_fill(t, m, k, d, NW_OUT_DIRS))) return done(rc);
         if ((rc = hipchk(hipMemsetAsync(ctl, 0, 64, t->stream), "hipMemset"))) return done(rc);
-        nw_first_path_kernel<<<1, 64, 0, t->stream>>>(t->D, t->lay_NC, t->skew, (int32_t)ie, (int32_t)nr, b == 0 ? 1 : 0,
-                                                      dmoves, ctl);
+        nw_first_path_kernel<<<1, 64, 0, t->stream>>>(t->D, t->lay_NC, t->skew, t->pair, (int32_t)ie, (int32_t)nr,
+                                                      b == 0 ? 1 : 0, dmoves, ctl);
         if ((rc = hipchk(hipGetLastError(), "first path kernel"))) return done(rc);
         uint32_t hc[8];
         if ((rc = hipchk(hipMemcpyAsync(hc, ctl, sizeof hc, hipMemcpyDeviceToHost, t->stream), "hipMemcpy")))

@@ -20,10 +20,10 @@ import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
 
-@pytest.fixture(params=["scan", "skew"], autouse=True)
+@pytest.fixture(params=["scan", "skew", "pair"], autouse=True)
 def fill_kernel(request, monkeypatch):
-    """Every test runs on both fill kernels (nw_fill.hip's column scan and
-    nw_skew.hip's skewed stripes), which write different device layouts."""
+    """Every test runs on every fill kernel (nw_fill.hip's column scan,
+    nw_skew.hip's skewed stripes, nw_pair.hip's two-row scan), whose device layouts differ."""
     monkeypatch.setenv("NW_KERNEL", request.param)
     return request.param
 

@@ -8,7 +8,7 @@ out=gpurun_out/ab_shapes_kernels.txt
 for spec in "$@"; do
   set -- $spec
   outs=$3; [ "$outs" = none ] && outs=""
-  for K in skew scan; do
+  for K in skew scan pair; do
     NW_KERNEL=$K timeout -k 10 200 python bench.py --no-cpu-baseline --steps 2 --warmup 1 --L1 $1 --L2 $2 --outputs "$outs" > gpurun_out/abk.log 2>&1
     python3 - "$K" "$1x$2" "$3" >> $out <<'PY'
 import json, sys
