@@ -58,9 +58,48 @@ __device__ __forceinline__ int prefmax(int x) {
 }
 
 __device__ __forceinline__ void pair_store_scores(const int* h, int32_t* p) {
-    typedef int v4i_ __attribute__((ext_vector_type(4)));
-    __builtin_nontemporal_store(v4i_{h[0], h[1], h[2], h[3]}, reinterpret_cast<v4i_*>(p));
-    __builtin_nontemporal_store(v4i_{h[4], h[5], h[6], h[7]}, reinterpret_cast<v4i_*>(p + 256));
+    __builtin_nontemporal_store(v4i{h[0], h[1], h[2], h[3]}, reinterpret_cast<v4i*>(p));
+    __builtin_nontemporal_store(v4i{h[4], h[5], h[6], h[7]}, reinterpret_cast<v4i*>(p + 256));
+}
+
+// Operands of the generated chunk block (nw_pair_chunk.inc).
+struct PairSlot {
+    v4i a, b;           // T (row above, G') of columns 0..3, 4..7 of the chunk
+    v2i c;              // the chunk's 8 top-string symbols
+};
+struct PairRegs {
+    int ga, gb;         // in/out: final G' of rows a, b at the previous / this chunk's last column
+    int sh;             // in/out: wave_shr1(gb), lane 0 = the row above at that column
+    int ha[8], hb[8];   // out: H of rows a, b
+    uint32_t accA, accB;// out: the chunk's code words of rows a, b
+    int gavA, gavB;     // in/out: running max |H| (stats)
+    uint64_t pq;        // out: {prog[w], cons[w+1]} read mid-chunk
+    int nloa, nlob;     // H = G' + nlo - (s+1)d (moved by -8d per chunk by the caller)
+};
+struct PairConst {
+    int kd[8];          // -(s+1)*d
+    uint32_t c2a, c2b;  // side symbols of rows a, b (byte compares)
+    int vcm, vck;       // sub' for match / mismatch
+    uint32_t pla, pha, plb, phb;   // profiles of rows a, b: byte q = sub' of symbol q (int8)
+    int cb;             // LDS address of ctr[2w]
+};
+
+#include "nw_pair_chunk.inc"
+
+// Slow path: {prog[w], cons[w+1]}, then the slot (in order per wave: slot
+// data read after a progress value that covers it is valid).  Waited for.
+__device__ __forceinline__ uint64_t pair_read_slot(int cb, int rd, PairSlot& s) {
+    uint64_t pq;
+    asm volatile(
+        "ds_read_b64 %[pq], %[cb] offset:8\n\t"
+        "ds_read_b128 %[a], %[rd]\n\t"
+        "ds_read_b128 %[b], %[rd] offset:16\n\t"
+        "ds_read_b64 %[c], %[rd] offset:32\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : [pq] "=&v"(pq), [a] "=&v"(s.a), [b] "=&v"(s.b), [c] "=&v"(s.c)
+        : [cb] "v"(cb), [rd] "v"(rd)
+        : "memory");
+    return pq;
 }
 
 template <int W, bool SH, bool SD, bool ST, bool PROF>
@@ -69,6 +108,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
     constexpr int NOCONS = 1 << 30;
     __shared__ __attribute__((aligned(16))) int tring[(W + 1) * R * SLOT];
     __shared__ __attribute__((aligned(8))) int ctr[2 * W + 4];
+    __shared__ int scratch[64 + R * SLOT];     // dummy target of the block's ring writes (lanes 0..62)
     __shared__ int sh_sidx;
     __shared__ int sh_abort;
 
@@ -195,38 +235,98 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
             const int* tin = &tring[w * R * SLOT];
             int* tout = &tring[(w + 1) * R * SLOT];
             const int* cin = &ctr[2 * w + 1];          // {cons[w], prog[w], cons[w+1]}
-            const uint32_t c2a = a.s2[ja - 1], c2b = a.s2[jb - 1];
+            PairConst kc;
+            kc.c2a = a.s2[ja - 1];
+            kc.c2b = a.s2[jb - 1];
+            kc.vcm = vcm;
+            kc.vck = vck;
+#pragma unroll
+            for (int s = 0; s < CH; ++s) {
+                kc.kd[s] = -(s + 1) * d;
+                asm volatile("" : "+v"(kc.kd[s]));     // keep the constants in VGPRs
+            }
+            asm volatile("" : "+v"(kc.c2a), "+v"(kc.c2b), "+v"(kc.vcm), "+v"(kc.vck));
+            kc.pla = kc.pha = kc.plb = kc.phb = 0;
+            if (PROF) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const uint32_t ba = (uint32_t)((uint32_t)q == kc.c2a ? vcm : vck) & 0xffu;
+                    const uint32_t bb = (uint32_t)((uint32_t)q == kc.c2b ? vcm : vck) & 0xffu;
+                    if (q < 4) {
+                        kc.pla |= ba << (8 * q);
+                        kc.plb |= bb << (8 * q);
+                    } else {
+                        kc.pha |= ba << (8 * (q - 4));
+                        kc.phb |= bb << (8 * (q - 4));
+                    }
+                }
+            }
+            kc.cb = lds_addr(&ctr[2 * w]);
+            asm volatile("" : "+v"(kc.cb));
+            // Ring writes of the block: lane 63 into the slot, the other lanes
+            // into a per-lane dummy (conflict-free, no exec juggling).
+            const int ring0 = lane == 63 ? lds_addr(tout) : lds_addr(&scratch[lane]);
+            int ra[R], rd[R];
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                ra[q] = ring0 + q * SLOT * 4;
+                rd[q] = lds_addr(tin) + q * SLOT * 4;
+                asm volatile("" : "+v"(ra[q]), "+v"(rd[q]));
+            }
             // column 0 (and the row above at column 0): G' = -(1 + row_base + 128*g0)*d
             const int C0 = -(1 + a.row_base + 128 * g0) * d;
-            int Ga = C0, Gb = C0, sh = C0;
-            int nloa = -(128 * w + 2 * lane) * d;      // H = G' + nlo - (s+1)d in chunk 0
-            uint32_t accpA = 0, accpB = 0;
+            PairRegs r;
+            r.ga = r.gb = r.sh = C0;
+            r.gavA = r.gavB = 0;
+            r.pq = 0;
+            r.nloa = -(128 * w + 2 * lane) * d;       // H = G' + nlo - (s+1)d in chunk 0
+            r.nlob = r.nloa - d;
             bool aborted = false;
             if (a.trace && lane == 0 && w == 0) {
                 a.trace[8 * (int64_t)sidx + 1] = __builtin_amdgcn_s_memrealtime();
                 a.trace[8 * (int64_t)sidx + 4] = __builtin_amdgcn_s_memtime();
             }
             if (a.trace && lane == 0 && w == nw - 1) a.trace[8 * (int64_t)sidx + 6] = __builtin_amdgcn_s_memrealtime();
-            for (int c = 0; c < NC && !aborted; ++c) {
+            auto rebase = [&](int c) {
                 if (c > 0 && c % SUPER_CHUNKS == 0) {
                     const int shv = SUPER_CHUNKS * CH * d;
-                    Ga -= shv;
-                    Gb -= shv;
-                    sh -= shv;
-                    nloa += shv;
+                    r.ga -= shv;
+                    r.gb -= shv;
+                    r.sh -= shv;
+                    r.nloa += shv;
+                    r.nlob += shv;
                 }
+            };
+            // Granules of chunk c: the WG-stripe's / panel's bottom row
+            // (plain domain: H - d = G' - 128(w+1)d - (i - base)d).
+            auto publish_vals = [&](int c, int n, int gv) {
+                if (lane < n) {
+                    const int v = gv - 128 * (w + 1) * d - (CH * c + lane + 1 - chunk_base(c)) * d;
+                    const uint64_t tag = publish ? (uint32_t)(sidx + 1) : a.epoch;
+                    const uint64_t gr = (tag << 32) | (uint32_t)v;
+                    if (publish)
+                        __hip_atomic_store(gout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    else
+                        __hip_atomic_store(a.xout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                if (xpublish && a.xflag && ((c + 1) % a.xblk == 0 || c == NC - 1)) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (lane == 0)
+                        __hip_atomic_store(&a.xflag[c / a.xblk], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            };
+            // ---- generic chunk (the last one: n = 1..8 columns) ----
+            auto generic_chunk = [&](int c) -> bool {
                 const int n = (c == NC - 1) ? nlast : CH;
                 for (;;) {
                     const int pin = uni(lds_ld(&cin[1]));
                     const int pout = uni(lds_ld(&cin[2]));
                     if (pin > c && pout >= c - R + 1) break;
-                    if (uni(lds_ld(&sh_abort))) {
-                        aborted = true;
-                        break;
-                    }
+                    if (uni(lds_ld(&sh_abort))) return false;
                     __builtin_amdgcn_s_sleep(1);
                 }
-                if (aborted) break;
                 lds_order();
                 const int* slot = &tin[(c % R) * SLOT];
                 int T[CH];
@@ -242,27 +342,27 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
                 for (int s = 0; s < CH; ++s) {
                     if (s < n) {
                         const uint32_t sym = (uint32_t)(sym8 >> (8 * s)) & 0xffu;
-                        const int dga = sh + (sym == c2a ? vcm : vck);
-                        const int Xa = max(max(Ga, dga), T[s]);
-                        const int dgb = Ga + (sym == c2b ? vcm : vck);
-                        const int Xb = max(max(Gb, dgb), Xa);
+                        const int dga = r.sh + (sym == kc.c2a ? vcm : vck);
+                        const int Xa = max(max(r.ga, dga), T[s]);
+                        const int dgb = r.ga + (sym == kc.c2b ? vcm : vck);
+                        const int Xb = max(max(r.gb, dgb), Xa);
                         const int Gbn = prefmax(Xb);
                         const int shn = shr1(T[s], Gbn);
                         const int Gan = max(Xa, shn);
-                        const uint32_t ca = (dga == Gan ? 1u : 0u) | (shn == Gan ? 2u : 0u) | (Ga == Gan ? 4u : 0u);
-                        const uint32_t cb = (dgb == Gbn ? 1u : 0u) | (Gan == Gbn ? 2u : 0u) | (Gb == Gbn ? 4u : 0u);
+                        const uint32_t ca = (dga == Gan ? 1u : 0u) | (shn == Gan ? 2u : 0u) | (r.ga == Gan ? 4u : 0u);
+                        const uint32_t cb = (dgb == Gbn ? 1u : 0u) | (Gan == Gbn ? 2u : 0u) | (r.gb == Gbn ? 4u : 0u);
                         accA = (accA << 3) | ca;
                         accB = (accB << 3) | cb;
-                        ha[s] = Gan + nloa - (s + 1) * d;
-                        hb[s] = Gbn + nloa - (s + 2) * d;
+                        ha[s] = Gan + r.nloa - (s + 1) * d;
+                        hb[s] = Gbn + r.nlob - (s + 1) * d;
                         if (ST) {
-                            if (okA) gav = max(gav, ha[s] < 0 ? -ha[s] : ha[s]);
-                            if (okB) gav = max(gav, hb[s] < 0 ? -hb[s] : hb[s]);
+                            r.gavA = max(r.gavA, ha[s] < 0 ? -ha[s] : ha[s]);
+                            r.gavB = max(r.gavB, hb[s] < 0 ? -hb[s] : hb[s]);
                         }
                         if (lane == 63) so[s] = Gbn;
-                        Ga = Gan;
-                        Gb = Gbn;
-                        sh = shn;
+                        r.ga = Gan;
+                        r.gb = Gbn;
+                        r.sh = shn;
                     } else {
                         ha[s] = hb[s] = 0;
                     }
@@ -291,32 +391,78 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
                     a.lastcol[ja] = ha[n - 1];
                     a.lastcol[jb] = hb[n - 1];
                 }
-                // (plain domain: H - d = G' - 128(w+1)d - (i - base)d)
-                if (publish || xpublish) {
-                    if (lane < n) {
-                        const int v = so[lane] - 128 * (w + 1) * d - (CH * c + lane + 1 - chunk_base(c)) * d;
-                        const uint64_t tag = publish ? (uint32_t)(sidx + 1) : a.epoch;
-                        const uint64_t gr = (tag << 32) | (uint32_t)v;
-                        if (publish)
-                            __hip_atomic_store(gout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        else
-                            __hip_atomic_store(a.xout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
-                    if (xpublish && a.xflag && ((c + 1) % a.xblk == 0 || c == NC - 1)) {
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        if (lane == 0)
-                            __hip_atomic_store(&a.xflag[c / a.xblk], a.epoch, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
-                }
+                if (publish || xpublish) publish_vals(c, n, tout[(c % R) * SLOT + lane]);
                 lds_order();
                 if (lane == 0) lds_publish(&ctr[2 * w + 4], c + 1);
-                nloa -= CH * d;
+                r.nloa -= CH * d;
+                r.nlob -= CH * d;
+                return true;
+            };
+            // ---- full chunks: the generated block (nw_pair_chunk.inc) ----
+            PairSlot tA, tB;
+            int pendv = 0;                             // lane < 8: chunk c-1's bottom-row values (publishers)
+            auto wait_slot = [&](int c, PairSlot& tt) -> bool {
+                for (;;) {
+                    const uint64_t pq = pair_read_slot(kc.cb, rd[c % R], tt);
+                    const int pin = uni((int)(uint32_t)pq), pout = uni((int)(pq >> 32));
+                    if (pin > c && pout >= c - R + 1) return true;
+                    if (uni(lds_ld(&sh_abort))) return false;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            };
+            auto full_chunk = [&](int c, auto slotc, const PairSlot& cur, PairSlot& nxt) -> bool {
+                constexpr int Q = decltype(slotc)::value;
+                pair_chunk_asm<ST, PROF>(r, kc, cur, nxt, c + 1, ra[Q], rd[(Q + 1) % R]);
+                if (SH) {
+                    pair_store_scores(r.ha, tileA + (int64_t)c * 512 + lane * 4);
+                    pair_store_scores(r.hb, tileB + (int64_t)c * 512 + lane * 4);
+                }
+                if (SD) {
+                    __builtin_nontemporal_store(r.accA, dtileA + (int64_t)(c + 1) * 64 + lane);
+                    __builtin_nontemporal_store(r.accB, dtileB + (int64_t)(c + 1) * 64 + lane);
+                }
+                if (ST) {
+                    bc += branch_codes(okA ? r.accA : 0u);
+                    bc += branch_codes(okB ? r.accB : 0u);
+                }
+                // granules one chunk late: the slot read issued now is done by
+                // the time they go out after the next block
+                if (publish || xpublish) {
+                    if (c > 0) publish_vals(c - 1, CH, pendv);
+                    pendv = tout[(c % R) * SLOT + lane];
+                }
+                r.nloa -= CH * d;
+                r.nlob -= CH * d;
+                if (c + 2 >= NC) return true;          // the next chunk is the generic last one
+                if (uni((int)(uint32_t)r.pq) > c + 1 && uni((int)(r.pq >> 32)) >= c + 2 - R) return true;
+                return wait_slot(c + 1, nxt);
+            };
+            using S0 = std::integral_constant<int, 0>;
+            using S1 = std::integral_constant<int, 1>;
+            using S2 = std::integral_constant<int, 2>;
+            using S3 = std::integral_constant<int, 3>;
+            int c = 0;
+            const int nfull = NC - 1;                  // chunks before the last one
+            if (nfull > 0) aborted = !wait_slot(0, tA);
+            while (c + R <= nfull && !aborted) {
+                rebase(c);
+                aborted = !full_chunk(c, S0{}, tA, tB) || !full_chunk(c + 1, S1{}, tB, tA) ||
+                          !full_chunk(c + 2, S2{}, tA, tB) || !full_chunk(c + 3, S3{}, tB, tA);
+                c += R;
             }
-            (void)accpA;
-            (void)accpB;
+            if (!aborted && c < nfull) {
+                rebase(c);
+                aborted = !full_chunk(c, S0{}, tA, tB);
+                if (!aborted && c + 1 < nfull) aborted = !full_chunk(c + 1, S1{}, tB, tA);
+                if (!aborted && c + 2 < nfull) aborted = !full_chunk(c + 2, S2{}, tA, tB);
+                c = nfull;
+            }
+            if (!aborted && nfull > 0 && (publish || xpublish)) publish_vals(nfull - 1, CH, pendv);
+            if (!aborted) {
+                rebase(c);
+                aborted = !generic_chunk(c);
+            }
+            if (ST) gav = max(okA ? r.gavA : 0, okB ? r.gavB : 0);
         }
         if (a.trace && !loader && w == nw - 1 && lane == 0) {
             a.trace[8 * (int64_t)sidx + 2] = __builtin_amdgcn_s_memrealtime();

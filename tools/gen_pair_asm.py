@@ -1,0 +1,292 @@
+#!/usr/bin/env python3
+"""Generate needleman-wunsch_amd/csrc/nw_pair_chunk.inc: the hand-scheduled
+8-column block of the two-rows-per-lane scan kernel (nw_pair.hip).
+
+    python tools/gen_pair_asm.py [--out PATH]
+
+Lane l holds rows a = 2l and b = 2l + 1 of a 128-row stripe.  Column step s
+(G' domain of nw_pair.hip; sh_s = wave_shr1(Gb_{s-1}) with lane 0 = T_{s-1}):
+
+    D   sh_s  = v_mov_b32_dpp Gb_{s-1} wave_shr:1   (lane 0 pre-filled with T_{s-1})
+    F   Ga_{s-1} = max(Xa_{s-1}, sh_s)              (row a of the previous column is final)
+    A1  dga_s = sh_s + sub'_a(s)                    (SDWA sext byte of the row-a profile)
+    A3  dgb_s = Ga_{s-1} + sub'_b(s)
+    A2  Xa_s  = max3(Ga_{s-1}, dga_s, T_s)
+    A4  Xb_s  = max3(Gb_{s-1}, dgb_s, Xa_s)
+    S1..S6  Gb_s = prefix max of Xb_s           (6 x v_max_i32_dpp in place)
+
+Step 0 takes sh_0, Ga_{-1}, Gb_{-1} from the previous block (its tail runs D
+and F for column 7).  Every DPP needs two instructions after the VALU that
+wrote its source; those gaps take the previous column's work: its two code
+words (candidate - G' is 0 exactly for the candidates that attain the max,
+so the sign bit of one v_sub is the inverted flag, shifted in with
+v_alignbit_b32), its scores H = G' + nlo + kd, the ring write of lane 63's
+Gb (the row above of the wave below), the lane-0 pre-fill of the next shift
+and the chunk's LDS traffic (cons, the next slot's {prog, cons}, 8 T and the
+chunk's symbols, the symbols down the ring, prog after the last ring write).
+The block ends with lgkmcnt(K), K = the LDS ops issued after its last read.
+
+Template pair_chunk_asm<ST, P>: ST = |H| max for the stats (rows a, b apart),
+P = profile lookups (symbols coded 0..7) instead of byte compares.
+"""
+import argparse
+import os
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+OUT = os.path.join(ROOT, "needleman-wunsch_amd", "csrc", "nw_pair_chunk.inc")
+
+
+def GA(s):
+    return "gac" if s in (-1, 7) else f"ga{s}"
+
+
+def GB(s):
+    return "gbc" if s in (-1, 7) else f"gb{s}"
+
+
+def SH(s):
+    return "shc" if s in (0, 8) else f"sh{s}"
+
+
+def XA(s):
+    return f"xa{s % 2}"
+
+
+def DGA(s):
+    return f"dga{s % 2}"
+
+
+def DGB(s):
+    return f"dgb{s % 2}"
+
+
+def T(s):
+    return f"ta{s}" if s < 4 else f"tb{s - 4}"
+
+
+class It:
+    def __init__(self, name, text, deps=(), lds=False):
+        self.name, self.text, self.deps, self.lds = name, text, list(deps), lds
+
+
+def sub_items(s, P, row):
+    """dg of row a (from sh_s) or b (from Ga_{s-1}) at step s."""
+    if row == "a":
+        dst, src, prof = DGA(s), SH(s), ("subA0" if s < 4 else "subA1")
+    else:
+        dst, src, prof = DGB(s), GA(s - 1), ("subB0" if s < 4 else "subB1")
+    if P:
+        return [f"v_add_u32_sdwa %[{dst}], %[{src}], sext(%[{prof}]) dst_sel:DWORD dst_unused:UNUSED_PAD "
+                f"src0_sel:DWORD src1_sel:BYTE_{s % 4}"]
+    w = "tc0" if s < 4 else "tc1"
+    c2 = "c2a" if row == "a" else "c2b"
+    return [f"v_cmp_eq_u32_sdwa vcc, %[{w}], %[{c2}] src0_sel:BYTE_{s % 4} src1_sel:DWORD",
+            "v_cndmask_b32_e64 %[sub], %[vck], %[vcm], vcc",
+            f"v_add_u32_e32 %[{dst}], %[{src}], %[sub]"]
+
+
+def column_items(c, ST, tail=False):
+    """Codes, scores, ring write of column c (needs Ga_c final: dep 'F')."""
+    its = []
+    # row b parts need no F
+    its.append(It("Lb", f"v_sub_u32_e32 %[dLb], %[{GB(c - 1)}], %[{GB(c)}]"))
+    its.append(It("Hb", f"v_add3_u32 %[hb{c}], %[{GB(c)}], %[nlob], %[kd{c}]"))
+    its.append(It("R", f"ds_write_b32 %[ra], %[{GB(c)}] offset:{4 * c}", lds=True))
+    its.append(It("Db", f"v_sub_u32_e32 %[dDb], %[{DGB(c)}], %[{GB(c)}]"))
+    its.append(It("Ub", f"v_sub_u32_e32 %[dUb], %[{GA(c)}], %[{GB(c)}]", ["F"]))
+    its.append(It("La", f"v_sub_u32_e32 %[dLa], %[{GA(c - 1)}], %[{GA(c)}]", ["F"]))
+    its.append(It("Ua", f"v_sub_u32_e32 %[dUa], %[{SH(c + 1)}], %[{GA(c)}]", ["F"]))
+    its.append(It("Da", f"v_sub_u32_e32 %[dDa], %[{DGA(c)}], %[{GA(c)}]", ["F"]))
+    its.append(It("Ha", f"v_add3_u32 %[ha{c}], %[{GA(c)}], %[nloa], %[kd{c}]", ["F"]))
+    hiA = "0" if c == 0 else "%[accA]"
+    hiB = "0" if c == 0 else "%[accB]"
+    its.append(It("bA1", f"v_alignbit_b32 %[accA], {hiA}, %[dLa], 31", ["La"]))
+    its.append(It("bB1", f"v_alignbit_b32 %[accB], {hiB}, %[dLb], 31", ["Lb"]))
+    its.append(It("bA2", "v_alignbit_b32 %[accA], %[accA], %[dUa], 31", ["Ua", "bA1"]))
+    its.append(It("bB2", "v_alignbit_b32 %[accB], %[accB], %[dUb], 31", ["Ub", "bB1"]))
+    its.append(It("bA3", "v_alignbit_b32 %[accA], %[accA], %[dDa], 31", ["Da", "bA2"]))
+    its.append(It("bB3", "v_alignbit_b32 %[accB], %[accB], %[dDb], 31", ["Db", "bB2"]))
+    if ST:
+        its.append(It("Za", f"v_sub_u32_e32 %[tmp], 0, %[ha{c}]", ["Ha"]))
+        its.append(It("Ma", f"v_max3_i32 %[gavA], %[gavA], %[ha{c}], %[tmp]", ["Za"]))
+        its.append(It("Zb", f"v_sub_u32_e32 %[tmp], 0, %[hb{c}]", ["Hb", "Ma"]))
+        its.append(It("Mb", f"v_max3_i32 %[gavB], %[gavB], %[hb{c}], %[tmp]", ["Zb"]))
+    return its
+
+
+def block(ST, P):
+    out = []          # list of It
+    done = set()
+
+    def emit(it):
+        out.append(it)
+        done.add(it.name)
+
+    def take(pool, k, ready):
+        got = []
+        for it in list(pool):
+            if len(got) == k:
+                break
+            if all(d_ in done or d_ in ready or d_ in [g.name for g in got] for d_ in it.deps):
+                got.append(it)
+                pool.remove(it)
+        return got
+
+    def gap(pool, ready=()):
+        got = take(pool, 2, ready)
+        for g in got:
+            emit(g)
+        if len(got) == 1:
+            out.append(It("", "s_nop 0"))
+        elif not got:
+            out.append(It("", "s_nop 1"))
+
+    mem = {0: [It("CW", "ds_write_b32 %[cb], %[cv] offset:4", lds=True),            # cons[w] = c+1
+               It("W8", "ds_write_b32 %[ra], %[tc0] offset:32", lds=True),          # symbols down the ring
+               It("W9", "ds_write_b32 %[ra], %[tc1] offset:36", lds=True)],
+           2: [It("PQ", "ds_read_b64 %[pq], %[cb] offset:8", lds=True)],             # {prog[w], cons[w+1]}
+           3: [It("TA", "ds_read_b128 %[nA], %[rd]", lds=True)],
+           4: [It("TB", "ds_read_b128 %[nB], %[rd] offset:16", lds=True)],
+           5: [It("TC", "ds_read_b64 %[nC], %[rd] offset:32", lds=True)]}
+    # head: profile lookups of the chunk, pre-fill of sh_1
+    if P:
+        out += [It("", "v_perm_b32 %[subA0], %[pha], %[pla], %[tc0]"),
+                It("", "v_perm_b32 %[subA1], %[pha], %[pla], %[tc1]"),
+                It("", "v_perm_b32 %[subB0], %[phb], %[plb], %[tc0]"),
+                It("", "v_perm_b32 %[subB1], %[phb], %[plb], %[tc1]")]
+    for s in range(8):
+        done.discard("F")
+        pool = []
+        if s > 0:
+            pool += column_items(s - 1, ST)
+        pool.append(It("P", f"v_mov_b32_e32 %[{SH(s + 1)}], %[{T(s)}]"))            # lane 0's next shift
+        pool += mem.get(s, [])
+        chain = []
+        if s > 0:
+            gap(pool)                                                              # D reads Gb_{s-1}
+            emit(It("D", f"v_mov_b32_dpp %[{SH(s)}], %[{GB(s - 1)}] wave_shr:1 row_mask:0xf bank_mask:0xf"))
+        for t in sub_items(s, P, "a"):
+            emit(It("A1", t))
+        if s > 0:
+            emit(It("F", f"v_max_i32_e32 %[{GA(s - 1)}], %[{XA(s - 1)}], %[{SH(s)}]"))
+        else:
+            done.add("F")
+        for t in sub_items(s, P, "b"):
+            emit(It("A3", t))
+        emit(It("A2", f"v_max3_i32 %[{XA(s)}], %[{GA(s - 1)}], %[{DGA(s)}], %[{T(s)}]"))
+        emit(It("A4", f"v_max3_i32 %[{GB(s)}], %[{GB(s - 1)}], %[{DGB(s)}], %[{XA(s)}]"))
+        dpps = ["row_shr:1 row_mask:0xf", "row_shr:2 row_mask:0xf", "row_shr:4 row_mask:0xf",
+                "row_shr:8 row_mask:0xf", "row_bcast:15 row_mask:0xa", "row_bcast:31 row_mask:0xc"]
+        g = GB(s)
+        for dp in dpps:
+            gap(pool)
+            emit(It("", f"v_max_i32_dpp %[{g}], %[{g}], %[{g}] {dp} bank_mask:0xf"))
+        while pool:
+            got = take(pool, 1, ())
+            assert got, [p.name for p in pool]
+            emit(got[0])
+    # tail: D and F of column 7, its codes / scores / ring write, then prog
+    done.discard("F")
+    pool = column_items(7, ST)
+    gap(pool)
+    emit(It("D", f"v_mov_b32_dpp %[{SH(8)}], %[{GB(7)}] wave_shr:1 row_mask:0xf bank_mask:0xf"))
+    emit(It("F", f"v_max_i32_e32 %[{GA(7)}], %[{XA(7)}], %[{SH(8)}]"))
+    while pool:
+        got = take(pool, 1, ())
+        assert got, [p.name for p in pool]
+        emit(got[0])
+    emit(It("", "v_xor_b32_e32 %[accA], 0xffffff, %[accA]"))                # flags were collected inverted
+    emit(It("", "v_xor_b32_e32 %[accB], 0xffffff, %[accB]"))
+    emit(It("PW", "ds_write_b32 %[cb], %[cv] offset:16", lds=True))         # prog[w+1] = c+1
+    lines = [it.text for it in out]
+    last = max(i for i, x in enumerate(lines) if x.startswith("ds_read"))
+    k = sum(1 for x in lines[last + 1:] if x.startswith("ds_"))
+    lines.append(f"s_waitcnt lgkmcnt({min(k, 15)})")
+    check(lines)
+    return lines
+
+
+def check(lines):
+    """DPP sources: two wait states (instructions, or s_nop N = N + 1) after the
+    VALU that wrote them."""
+    def dst(x):
+        if x.startswith(("ds_", "s_")):
+            return None
+        return x.split()[1].rstrip(",")
+
+    def states(x):
+        return int(x.split()[1]) + 1 if x.startswith("s_nop") else 1
+    for i, x in enumerate(lines):
+        if "_dpp" in x:
+            src = x.split()[2].rstrip(",")
+            ws = 0
+            for j in range(i - 1, -1, -1):
+                if dst(lines[j]) == src:
+                    assert ws >= 2, (i, x, lines[j])
+                    break
+                ws += states(lines[j])
+                if ws >= 2:
+                    break
+
+
+OPERANDS = r'''
+#define NW_PAIR_OPERANDS                                                                                   \
+    : [ga0] "=&v"(ga_[0]), [ga1] "=&v"(ga_[1]), [ga2] "=&v"(ga_[2]), [ga3] "=&v"(ga_[3]),                  \
+      [ga4] "=&v"(ga_[4]), [ga5] "=&v"(ga_[5]), [ga6] "=&v"(ga_[6]), [gac] "+v"(r.ga),                     \
+      [gb0] "=&v"(gb_[0]), [gb1] "=&v"(gb_[1]), [gb2] "=&v"(gb_[2]), [gb3] "=&v"(gb_[3]),                  \
+      [gb4] "=&v"(gb_[4]), [gb5] "=&v"(gb_[5]), [gb6] "=&v"(gb_[6]), [gbc] "+v"(r.gb),                     \
+      [sh1] "=&v"(sh_[1]), [sh2] "=&v"(sh_[2]), [sh3] "=&v"(sh_[3]), [sh4] "=&v"(sh_[4]),                  \
+      [sh5] "=&v"(sh_[5]), [sh6] "=&v"(sh_[6]), [sh7] "=&v"(sh_[7]), [shc] "+v"(r.sh),                     \
+      [xa0] "=&v"(xa_[0]), [xa1] "=&v"(xa_[1]), [dga0] "=&v"(dga_[0]), [dga1] "=&v"(dga_[1]),              \
+      [dgb0] "=&v"(dgb_[0]), [dgb1] "=&v"(dgb_[1]),                                                        \
+      [dLa] "=&v"(t_[0]), [dUa] "=&v"(t_[1]), [dDa] "=&v"(t_[2]), [dLb] "=&v"(t_[3]), [dUb] "=&v"(t_[4]),   \
+      [dDb] "=&v"(t_[5]), [tmp] "=&v"(t_[6]), [sub] "=&v"(t_[7]),                                          \
+      [subA0] "=&v"(sp_[0]), [subA1] "=&v"(sp_[1]), [subB0] "=&v"(sp_[2]), [subB1] "=&v"(sp_[3]),          \
+      [ha0] "=&v"(r.ha[0]), [ha1] "=&v"(r.ha[1]), [ha2] "=&v"(r.ha[2]), [ha3] "=&v"(r.ha[3]),              \
+      [ha4] "=&v"(r.ha[4]), [ha5] "=&v"(r.ha[5]), [ha6] "=&v"(r.ha[6]), [ha7] "=&v"(r.ha[7]),              \
+      [hb0] "=&v"(r.hb[0]), [hb1] "=&v"(r.hb[1]), [hb2] "=&v"(r.hb[2]), [hb3] "=&v"(r.hb[3]),              \
+      [hb4] "=&v"(r.hb[4]), [hb5] "=&v"(r.hb[5]), [hb6] "=&v"(r.hb[6]), [hb7] "=&v"(r.hb[7]),              \
+      [accA] "=&v"(r.accA), [accB] "=&v"(r.accB), [gavA] "+v"(r.gavA), [gavB] "+v"(r.gavB),                 \
+      [pq] "=&v"(r.pq), [nA] "=&v"(ns.a), [nB] "=&v"(ns.b), [nC] "=&v"(ns.c)                               \
+    : [ta0] "v"(ts.a[0]), [ta1] "v"(ts.a[1]), [ta2] "v"(ts.a[2]), [ta3] "v"(ts.a[3]),                      \
+      [tb0] "v"(ts.b[0]), [tb1] "v"(ts.b[1]), [tb2] "v"(ts.b[2]), [tb3] "v"(ts.b[3]),                      \
+      [tc0] "v"(ts.c[0]), [tc1] "v"(ts.c[1]),                                                              \
+      [kd0] "v"(k.kd[0]), [kd1] "v"(k.kd[1]), [kd2] "v"(k.kd[2]), [kd3] "v"(k.kd[3]),                      \
+      [kd4] "v"(k.kd[4]), [kd5] "v"(k.kd[5]), [kd6] "v"(k.kd[6]), [kd7] "v"(k.kd[7]),                      \
+      [nloa] "v"(r.nloa), [nlob] "v"(r.nlob), [c2a] "v"(k.c2a), [c2b] "v"(k.c2b), [vcm] "v"(k.vcm),         \
+      [vck] "v"(k.vck), [pla] "v"(k.pla), [pha] "v"(k.pha), [plb] "v"(k.plb), [phb] "v"(k.phb),             \
+      [cb] "v"(k.cb), [cv] "v"(cv), [ra] "v"(ra), [rd] "v"(rd)
+'''
+
+
+def cstr(lines):
+    return "\n".join(f'        "{ln}\\n\\t"' for ln in lines)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=OUT)
+    args = ap.parse_args()
+    parts = ["// GENERATED by tools/gen_pair_asm.py -- do not edit; see the generator for the schedule.\n",
+             OPERANDS,
+             "template <bool ST, bool P>\n"
+             "__device__ __forceinline__ void pair_chunk_asm(PairRegs& r, const PairConst& k, const PairSlot& ts,\n"
+             "                                               PairSlot& ns, int cv, int ra, int rd);\n"]
+    decl = "    int ga_[7], gb_[7], sh_[8], xa_[2], dga_[2], dgb_[2], t_[8], sp_[4];\n"
+    tf = lambda b: "true" if b else "false"
+    for ST in (0, 1):
+        for P in (0, 1):
+            lines = block(ST, P)
+            parts.append(
+                f"template <> __device__ __forceinline__ void pair_chunk_asm<{tf(ST)}, {tf(P)}>"
+                f"(PairRegs& r, const PairConst& k, const PairSlot& ts, PairSlot& ns, int cv, int ra, int rd) {{\n"
+                f"{decl}    asm volatile(\n{cstr(lines)}\n"
+                f"        NW_PAIR_OPERANDS : \"vcc\", \"memory\");\n}}\n")
+    parts.append("#undef NW_PAIR_OPERANDS\n")
+    with open(args.out, "w") as f:
+        f.write("\n".join(parts))
+    print("wrote", args.out)
+
+
+if __name__ == "__main__":
+    main()

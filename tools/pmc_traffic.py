@@ -25,7 +25,11 @@ import shutil
 import sys
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-FILL = "nw_fill_kernel"
+FILL_KERNELS = ("nw_fill_kernel", "nw_skew_kernel", "nw_pair_kernel")   # whichever fill ran
+
+
+def is_fill(name):
+    return any(k in name for k in FILL_KERNELS)
 
 
 def find(d, pattern):
@@ -40,7 +44,7 @@ def counter_per_launch(d, name):
     per = {}
     with open(path) as f:
         for r in csv.DictReader(f):
-            if FILL not in r["Kernel_Name"] or r["Counter_Name"] != name:
+            if not is_fill(r["Kernel_Name"]) or r["Counter_Name"] != name:
                 continue
             key = r.get("Dispatch_Id") or r.get("Correlation_Id")
             per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
@@ -58,7 +62,7 @@ def main():
     avg_ns = None
     with open(stats) as f:
         for r in csv.DictReader(f):
-            if FILL in r["Name"]:
+            if is_fill(r["Name"]):
                 avg_ns = float(r["AverageNs"])
                 name = r["Name"]
     wr_kib, nw, wsrc = counter_per_launch(os.path.join(out, "wr"), "WRITE_SIZE")
