@@ -718,18 +718,20 @@ struct StripePlan {
     int SQ, SR;         // see FillArgs
 };
 
-StripePlan plan_stripes(int64_t NG, int ncu) {
+// wmax: the most compute waves the kernel takes (the pair kernel adds a
+// publisher wave to the loader, so it stops at 12).
+StripePlan plan_stripes(int64_t NG, int ncu, int wmax = 15) {
     StripePlan p{8, (NG + 7) / 8, 8, 0};
     if (const char* e = getenv("NW_WAVES")) {
         const int w = atoi(e);
         for (int c : kWaveChoices)
-            if (c == w) return StripePlan{w, (NG + w - 1) / w, w, 0};
+            if (c == w && c <= wmax) return StripePlan{w, (NG + w - 1) / w, w, 0};
     }
     if (NG <= ncu) return StripePlan{1, NG, 1, 0};
     const int SQ = (int)(NG / ncu), SR = (int)(NG % ncu);
     const int need = SQ + (SR > 0);
     for (int c : kWaveChoices)
-        if (c >= need) return StripePlan{c, ncu, SQ, SR};
+        if (c >= need && c <= wmax) return StripePlan{c, ncu, SQ, SR};
     return p;
 }
 
@@ -819,7 +821,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         if (pair && t->xout && L2 % 128 != 0) pair = false;
         const int64_t NGk = pair ? (L2 + 127) / 128 : t->NG;
         if (pair) {
-            plan = plan_stripes(NGk, t->ncu);
+            plan = plan_stripes(NGk, t->ncu, 12);
             W = plan.W;
         }
         KernelFn fn = skew ? pick_skew(W, prof, sh, sd, stt)
@@ -871,7 +873,8 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
             a.trace = t->trace;
         }
         int occ = 1;
-        NW_HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(fn), 64 * (W + 1), 0));
+        const int wgw = W + (pair ? 2 : 1);   // + loader (+ publisher: nw_pair.hip)
+        NW_HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(fn), 64 * wgw, 0));
         occ = std::max(occ, 1);
         // A panel leaves room on every CU for the kernels of its neighbours
         // and of the transport (RCCL), which its hand-off waits on.
@@ -889,7 +892,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         if (a.NSW > 1) NW_HIPCHK(hipMemsetAsync(t->gran, 0, (size_t)a.nslot * a.gpitch * 8, t->stream));
         NW_HIPCHK(hipEventRecord(t->ev[1], t->stream));
         void* kargs[] = {&a};
-        NW_HIPCHK(hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3((unsigned)grid), dim3(64 * (W + 1)), kargs,
+        NW_HIPCHK(hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3((unsigned)grid), dim3(64 * wgw), kargs,
                                   0, t->stream));
         NW_HIPCHK(hipGetLastError());
         NW_HIPCHK(hipEventRecord(t->ev[2], t->stream));

@@ -102,8 +102,9 @@ __device__ __forceinline__ uint64_t pair_read_slot(int cb, int rd, PairSlot& s) 
     return pq;
 }
 
+// Workgroup = W compute waves + the loader + the publisher (<= 16 waves).
 template <int W, bool SH, bool SD, bool ST, bool PROF>
-__global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
+__global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
     constexpr int R = 4;
     constexpr int NOCONS = 1 << 30;
     __shared__ __attribute__((aligned(16))) int tring[(W + 1) * R * SLOT];
@@ -114,7 +115,8 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
 
     const int lane = threadIdx.x & 63;
     const int w = uni(threadIdx.x >> 6);
-    const bool loader = (w == W);
+    const bool loader = (w == W);          // feeds ring 0
+    const bool pubw = (w == W + 1);        // drains the last compute wave's ring into granules
     const int d = a.d;
     const int vcm = a.m + 2 * a.d;
     const int vck = 2 * a.d - a.k;
@@ -127,9 +129,10 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
             sh_sidx = sidx;
             sh_abort = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - (sidx * a.SQ + min(sidx, a.SR)));
+            const bool drain = sidx + 1 < a.NSW || (a.xout && sidx * a.SQ + min(sidx, a.SR) + nw - 1 == a.NG - 1);
             for (int v = 0; v <= W; ++v) {
                 ctr[2 * v + 2] = 0;
-                ctr[2 * v + 1] = v < nw ? 0 : NOCONS;
+                ctr[2 * v + 1] = v < nw || (v == nw && drain) ? 0 : NOCONS;   // the loader drains ring nw
             }
         }
         __syncthreads();
@@ -142,13 +145,56 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
         const int g0 = sidx * a.SQ + min(sidx, a.SR);                 // first pair stripe of the WG-stripe
         const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - g0);
         const int g = g0 + w;
-        const bool real = !loader && w < nw;
+        const bool real = w < nw;
         const int j0 = 1 + 128 * g;                // first row of the pair stripe
         const int ja = j0 + 2 * lane, jb = ja + 1; // this lane's rows
         int gav = 0;
         uint32_t bc = 0;
 
-        if (loader) {
+        if (pubw) {
+            // ---------------- publisher wave ----------------
+            // Drains the ring below the last compute wave into this
+            // WG-stripe's bottom-row granules (for the next WG-stripe, or the
+            // panel below), so the hand-off stores stay off the compute waves.
+            const bool publish = sidx + 1 < a.NSW;
+            // the panel's last row is row b of lane 63 of its last pair stripe (128*k rows)
+            const bool xpublish = a.xout && g0 + nw - 1 == a.NG - 1;
+            uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
+            const int* bot = &tring[nw * R * SLOT];
+            int cd = 0;
+            while ((publish || xpublish) && cd < NC) {
+                const int p = uni(lds_ld(&ctr[2 * nw + 2]));          // prog of the last wave's ring
+                if (p <= cd) {
+                    if (uni(lds_ld(&sh_abort))) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                lds_order();
+                for (; cd < p; ++cd) {
+                    const int n = (cd == NC - 1) ? nlast : CH;
+                    if (lane < n) {
+                        // (plain domain: H - d = G' - 128*nw*d - (i - base)d)
+                        const int v = bot[(cd % R) * SLOT + lane] - 128 * nw * d - (CH * cd + lane + 1 - chunk_base(cd)) * d;
+                        const uint64_t tag = publish ? (uint32_t)(sidx + 1) : a.epoch;
+                        const uint64_t gr = (tag << 32) | (uint32_t)v;
+                        if (publish)
+                            __hip_atomic_store(gout + CH * (int64_t)cd + lane, gr, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        else
+                            __hip_atomic_store(a.xout + CH * (int64_t)cd + lane, gr, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                    if (xpublish && a.xflag && ((cd + 1) % a.xblk == 0 || cd == NC - 1)) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the block is out before its flag
+                        if (lane == 0)
+                            __hip_atomic_store(&a.xflag[cd / a.xblk], a.epoch, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                }
+                lds_order();
+                if (lane == 0) lds_publish(&ctr[2 * nw + 1], cd);        // those ring slots are free again
+            }
+        } else         if (loader) {
             // ---------------- loader wave: ring 0 (as the one-row kernel's) ----------------
             const bool seeded = sidx == 0 && !a.xin;
             const bool xsrc = sidx == 0 && a.xin;
@@ -222,15 +268,11 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
             }
         } else if (real) {
             // ---------------- compute wave: its 128-row stripe, chunk by chunk ----
-            uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
             // virtual 64-row stripes 2g (rows a) and 2g+1 (rows b): a.spitch = 1024*NC
             int32_t* tileA = a.H + (int64_t)g * a.spitch;
             int32_t* tileB = tileA + a.spitch / 2;
             uint32_t* dtileA = a.D + (int64_t)(2 * g) * (NC + 1) * 64;
             uint32_t* dtileB = dtileA + (int64_t)(NC + 1) * 64;
-            const bool publish = (w == nw - 1) && sidx + 1 < a.NSW;
-            // the panel's last row is row b of lane 63 (feeding panels have 128*k rows)
-            const bool xpublish = a.xout && g == a.NG - 1;
             const bool okA = ja <= a.L2, okB = jb <= a.L2;
             const int* tin = &tring[w * R * SLOT];
             int* tout = &tring[(w + 1) * R * SLOT];
@@ -295,26 +337,6 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
                     r.sh -= shv;
                     r.nloa += shv;
                     r.nlob += shv;
-                }
-            };
-            // Granules of chunk c: the WG-stripe's / panel's bottom row
-            // (plain domain: H - d = G' - 128(w+1)d - (i - base)d).
-            auto publish_vals = [&](int c, int n, int gv) {
-                if (lane < n) {
-                    const int v = gv - 128 * (w + 1) * d - (CH * c + lane + 1 - chunk_base(c)) * d;
-                    const uint64_t tag = publish ? (uint32_t)(sidx + 1) : a.epoch;
-                    const uint64_t gr = (tag << 32) | (uint32_t)v;
-                    if (publish)
-                        __hip_atomic_store(gout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                    else
-                        __hip_atomic_store(a.xout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-                if (xpublish && a.xflag && ((c + 1) % a.xblk == 0 || c == NC - 1)) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (lane == 0)
-                        __hip_atomic_store(&a.xflag[c / a.xblk], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
             };
             // ---- generic chunk (the last one: n = 1..8 columns) ----
@@ -391,7 +413,6 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
                     a.lastcol[ja] = ha[n - 1];
                     a.lastcol[jb] = hb[n - 1];
                 }
-                if (publish || xpublish) publish_vals(c, n, tout[(c % R) * SLOT + lane]);
                 lds_order();
                 if (lane == 0) lds_publish(&ctr[2 * w + 4], c + 1);
                 r.nloa -= CH * d;
@@ -400,7 +421,6 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
             };
             // ---- full chunks: the generated block (nw_pair_chunk.inc) ----
             PairSlot tA, tB;
-            int pendv = 0;                             // lane < 8: chunk c-1's bottom-row values (publishers)
             auto wait_slot = [&](int c, PairSlot& tt) -> bool {
                 for (;;) {
                     const uint64_t pq = pair_read_slot(kc.cb, rd[c % R], tt);
@@ -424,12 +444,6 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
                 if (ST) {
                     bc += branch_codes(okA ? r.accA : 0u);
                     bc += branch_codes(okB ? r.accB : 0u);
-                }
-                // granules one chunk late: the slot read issued now is done by
-                // the time they go out after the next block
-                if (publish || xpublish) {
-                    if (c > 0) publish_vals(c - 1, CH, pendv);
-                    pendv = tout[(c % R) * SLOT + lane];
                 }
                 r.nloa -= CH * d;
                 r.nlob -= CH * d;
@@ -457,14 +471,13 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_pair_kernel(FillArgs a) {
                 if (!aborted && c + 2 < nfull) aborted = !full_chunk(c + 2, S2{}, tA, tB);
                 c = nfull;
             }
-            if (!aborted && nfull > 0 && (publish || xpublish)) publish_vals(nfull - 1, CH, pendv);
             if (!aborted) {
                 rebase(c);
                 aborted = !generic_chunk(c);
             }
             if (ST) gav = max(okA ? r.gavA : 0, okB ? r.gavB : 0);
         }
-        if (a.trace && !loader && w == nw - 1 && lane == 0) {
+        if (a.trace && real && w == nw - 1 && lane == 0) {
             a.trace[8 * (int64_t)sidx + 2] = __builtin_amdgcn_s_memrealtime();
             a.trace[8 * (int64_t)sidx + 5] = __builtin_amdgcn_s_memtime();
         }
@@ -512,8 +525,7 @@ KernelFn pick_pair(int W, bool prof, bool sh, bool sd, bool stt) {
         case 8: return pick_prof<8>(prof, sh, sd, stt);
         case 10: return pick_prof<10>(prof, sh, sd, stt);
         case 12: return pick_prof<12>(prof, sh, sd, stt);
-        case 15: return pick_prof<15>(prof, sh, sd, stt);
-        default: return nullptr;
+        default: return nullptr;   // (W + 2 waves <= 16)
     }
 }
 
