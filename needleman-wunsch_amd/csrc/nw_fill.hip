@@ -198,7 +198,7 @@ __device__ __forceinline__ void store_chunk_scores(const ChunkRegs& r, const Chu
 // Granules (between workgroups and panels) carry H - d of the row above in
 // the plain domain; ring slots carry G'.
 template <int W, bool SH, bool SD, bool ST, bool PROF>
-__global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
+__global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
     constexpr int R = 4;
     constexpr bool F = SD || ST;     // direction codes
     constexpr int NOCONS = 1 << 30;
@@ -214,7 +214,8 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
 
     const int lane = threadIdx.x & 63;
     const int w = uni(threadIdx.x >> 6);
-    const bool loader = (w == W);
+    const bool loader = (w == W);          // feeds ring 0
+    const bool pubw = (w == W + 1);        // drains the last compute wave's ring into granules
     const int d = a.d;
     int vcm = a.m + 2 * a.d;
     int vck = 2 * a.d - a.k;
@@ -236,9 +237,10 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             sh_sidx = sidx;
             sh_abort = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - (sidx * a.SQ + min(sidx, a.SR)));
+            const bool drain = sidx + 1 < a.NSW || (a.xout && sidx * a.SQ + min(sidx, a.SR) + nw - 1 == a.NG - 1);
             for (int v = 0; v <= W; ++v) {
                 ctr[2 * v + 2] = 0;
-                ctr[2 * v + 1] = v < nw ? 0 : NOCONS;
+                ctr[2 * v + 1] = v < nw || (v == nw && drain) ? 0 : NOCONS;   // the publisher drains ring nw
             }
         }
         __syncthreads();
@@ -252,13 +254,57 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
         const int g0 = sidx * a.SQ + min(sidx, a.SR);                 // first stripe of the WG-stripe
         const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - g0);  // its stripes (<= W)
         const int g = g0 + w;                      // wave stripe (compute waves)
-        const bool real = !loader && w < nw;
+        const bool real = w < nw;                  // (the loader and the publisher are waves W, W+1)
         const int j0 = 1 + 64 * g;                 // first row of the wave stripe
         const int jrow = j0 + lane;
         int gav = 0;
         uint32_t bc = 0;
 
-        if (loader) {
+        if (pubw) {
+            // ---------------- publisher wave ----------------
+            // Drains the ring below the last compute wave into this
+            // WG-stripe's bottom-row granules (for the next WG-stripe, or the
+            // panel below), so the hand-off stores stay off the compute waves
+            // (the stripe chain would otherwise move at the pace of each
+            // WG-stripe's publishing wave).
+            const bool publish = sidx + 1 < a.NSW;
+            const bool xpublish = a.xout && g0 + nw - 1 == a.NG - 1;
+            uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
+            const int* bot = &tring[nw * R * SLOT];
+            int cd = 0;
+            while ((publish || xpublish) && cd < NC) {
+                const int p = uni(lds_ld(&ctr[2 * nw + 2]));          // prog of the last wave's ring
+                if (p <= cd) {
+                    if (uni(lds_ld(&sh_abort))) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                lds_order();
+                for (; cd < p; ++cd) {
+                    const int n = (cd == NC - 1) ? nlast : CH;
+                    if (lane < n) {
+                        // (plain domain: H - d = G' - 64*nw*d - (i - base)d)
+                        const int v = bot[(cd % R) * SLOT + lane] - 64 * nw * d - (CH * cd + lane + 1 - chunk_base(cd)) * d;
+                        const uint64_t tag = publish ? (uint32_t)(sidx + 1) : a.epoch;
+                        const uint64_t gr = (tag << 32) | (uint32_t)v;
+                        if (publish)
+                            __hip_atomic_store(gout + CH * (int64_t)cd + lane, gr, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        else
+                            __hip_atomic_store(a.xout + CH * (int64_t)cd + lane, gr, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                    if (xpublish && a.xflag && ((cd + 1) % a.xblk == 0 || cd == NC - 1)) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the block is out before its flag
+                        if (lane == 0)
+                            __hip_atomic_store(&a.xflag[cd / a.xblk], a.epoch, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                }
+                lds_order();
+                if (lane == 0) lds_publish(&ctr[2 * nw + 1], cd);        // those ring slots are free again
+            }
+        } else if (loader) {
             // ---------------- loader wave: no stores, exact waits ----------------
             // Source of the WG-stripe's top row: the seeded row 0, the panel
             // above (xin, written by another agent: system-scope loads), or
@@ -341,15 +387,10 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             }
         } else if (real) {
             // ---------------- compute wave: its 64-row stripe, chunk by chunk ----
-            uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
             int32_t* tile = a.H + (int64_t)g * a.spitch;
             // codes: row q+1 of the stripe's code tile holds chunk q (row 0 pads
             // the block's store of the word "before" chunk 0)
             uint32_t* dtile = a.D + (int64_t)g * (NC + 1) * 64;
-            const bool publish = (w == nw - 1) && sidx + 1 < a.NSW;
-            // The wave holding the panel's last row (lane 63: panels above the
-            // last one have a multiple of 64 rows) feeds the panel below.
-            const bool xpublish = a.xout && g == a.NG - 1;
             const bool out_lane = jrow <= a.L2;
             const int* tin = &tring[w * R * SLOT];
             const int* tout = &tring[(w + 1) * R * SLOT];
@@ -448,28 +489,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
                     if (SD) dtile[(int64_t)(c + 1) * 64 + lane] = dw;
                     if (ST) bc += branch_codes(out_lane ? dw : 0u);
                 }
-                // (plain domain: H - d = G' - 64(w+1)d - (i - base)d)
-                if (publish || xpublish) {
-                    if (lane < n) {
-                        const int v = tout[slot * SLOT + lane] - 64 * (w + 1) * d -
-                                      (CH * c + lane + 1 - chunk_base(c)) * d;
-                        const uint64_t tag = publish ? (uint32_t)(sidx + 1) : a.epoch;
-                        const uint64_t gr = (tag << 32) | (uint32_t)v;
-                        if (publish)
-                            __hip_atomic_store(gout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        else
-                            __hip_atomic_store(a.xout + CH * (int64_t)c + lane, gr, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
-                    if (xpublish && a.xflag && ((c + 1) % a.xblk == 0 || last)) {
-                        // block complete: its granules are out before the flag
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        if (lane == 0)
-                            __hip_atomic_store(&a.xflag[c / a.xblk], a.epoch, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
-                }
+                (void)slot;
             };
             // One full (non-final) chunk; SLOTC = c % R is a compile-time ring
             // slot.  The block reads the next slot into nxt; the slow path
@@ -531,7 +551,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_fill_kernel(FillArgs a) {
             }
             gav = r.gav;
         }
-        if (a.trace && !loader && w == nw - 1 && lane == 0) {
+        if (a.trace && real && w == nw - 1 && lane == 0) {
             a.trace[8 * (int64_t)sidx + 2] = __builtin_amdgcn_s_memrealtime();
             a.trace[8 * (int64_t)sidx + 5] = __builtin_amdgcn_s_memtime();
         }
@@ -700,8 +720,7 @@ KernelFn pick_kernel(int W, bool prof, bool sh, bool sd, bool stt) {
         case 8: return pick_prof<8>(prof, sh, sd, stt);
         case 10: return pick_prof<10>(prof, sh, sd, stt);
         case 12: return pick_prof<12>(prof, sh, sd, stt);
-        case 15: return pick_prof<15>(prof, sh, sd, stt);
-        default: return nullptr;
+        default: return nullptr;   // (W + loader + publisher <= 16 waves)
     }
 }
 
@@ -786,7 +805,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
     int W = 0;
     bool skew = false, pair = false;
     if (L1 > 0 && L2 > 0) {
-        StripePlan plan = plan_stripes(t->NG, t->ncu);
+        StripePlan plan = plan_stripes(t->NG, t->ncu, 12);
         W = plan.W;
         // Profile lookups when the sequences were coded to <= 8 symbols and
         // sub' fits a signed byte ($NW_PROF=0 forces the byte compares).
@@ -873,7 +892,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
             a.trace = t->trace;
         }
         int occ = 1;
-        const int wgw = W + (pair ? 2 : 1);   // + loader (+ publisher: nw_pair.hip)
+        const int wgw = W + (skew ? 1 : 2);   // + loader (+ publisher: scan and pair kernels)
         NW_HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(fn), 64 * wgw, 0));
         occ = std::max(occ, 1);
         // A panel leaves room on every CU for the kernels of its neighbours
