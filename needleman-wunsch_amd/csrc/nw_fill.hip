@@ -826,14 +826,14 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         else if (ke && std::strcmp(ke, "scan") == 0) skew = false;
         else if (ke && std::strcmp(ke, "pair") == 0) pair = true;
         else {
-            // auto (profiles/r01_ab_skew_vs_scan_shapes.txt, r01_ab_pair_shapes.txt):
+            // auto (profiles/r01_ab_skew_vs_scan_shapes.txt,
+            // r01_ab_kernels_after_publisher.txt, r01_ab_pair_scoreonly.txt):
             // the pair kernel once the 64-row stripes outnumber the SIMDs (the
-            // scan kernel then doubles up waves and runs at the two-wave rate)
-            // and the fill writes outputs, or at twice that in score-only mode
-            // (its block always computes codes); the skew kernel for wide
-            // tables with few stripes; the scan kernel otherwise.
+            // scan kernel then doubles up waves and runs at the two-wave
+            // rate); the skew kernel for wide tables with few stripes; the
+            // scan kernel otherwise.
             const int64_t simds = 4 * (int64_t)t->ncu;
-            pair = t->NG > 2 * simds || (t->NG > simds && (sh || sd));
+            pair = t->NG > simds;
             skew = !pair && t->NG <= simds && L1 >= 4 * L2;
         }
         // a feeding panel's last row must be lane 63's row b of its last pair stripe

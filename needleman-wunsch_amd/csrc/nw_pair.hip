@@ -432,7 +432,7 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
             };
             auto full_chunk = [&](int c, auto slotc, const PairSlot& cur, PairSlot& nxt) -> bool {
                 constexpr int Q = decltype(slotc)::value;
-                pair_chunk_asm<ST, PROF>(r, kc, cur, nxt, c + 1, ra[Q], rd[(Q + 1) % R]);
+                pair_chunk_asm<SH || ST, SD || ST, ST, PROF>(r, kc, cur, nxt, c + 1, ra[Q], rd[(Q + 1) % R]);
                 if (SH) {
                     pair_store_scores(r.ha, tileA + (int64_t)c * 512 + lane * 4);
                     pair_store_scores(r.hb, tileB + (int64_t)c * 512 + lane * 4);

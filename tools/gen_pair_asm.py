@@ -26,8 +26,10 @@ and the chunk's LDS traffic (cons, the next slot's {prog, cons}, 8 T and the
 chunk's symbols, the symbols down the ring, prog after the last ring write).
 The block ends with lgkmcnt(K), K = the LDS ops issued after its last read.
 
-Template pair_chunk_asm<ST, P>: ST = |H| max for the stats (rows a, b apart),
-P = profile lookups (symbols coded 0..7) instead of byte compares.
+Template pair_chunk_asm<HH, FF, ST, P>: HH = scores, FF = direction codes
+(score-only fills skip both), ST = |H| max for the stats (rows a, b apart;
+needs HH and FF), P = profile lookups (symbols coded 0..7) instead of byte
+compares.
 """
 import argparse
 import os
@@ -85,8 +87,14 @@ def sub_items(s, P, row):
             f"v_add_u32_e32 %[{dst}], %[{src}], %[sub]"]
 
 
-def column_items(c, ST, tail=False):
-    """Codes, scores, ring write of column c (needs Ga_c final: dep 'F')."""
+def column_items(c, ST, HH=True, FF=True):
+    """Codes (FF), scores (HH), ring write of column c (needs Ga_c final: dep 'F')."""
+    its = [It("R", f"ds_write_b32 %[ra], %[{GB(c)}] offset:{4 * c}", lds=True)]
+    if not HH and not FF:
+        return its
+    if not FF:
+        return its + [It("Hb", f"v_add3_u32 %[hb{c}], %[{GB(c)}], %[nlob], %[kd{c}]"),
+                      It("Ha", f"v_add3_u32 %[ha{c}], %[{GA(c)}], %[nloa], %[kd{c}]", ["F"])]
     its = []
     # row b parts need no F
     its.append(It("Lb", f"v_sub_u32_e32 %[dLb], %[{GB(c - 1)}], %[{GB(c)}]"))
@@ -114,7 +122,7 @@ def column_items(c, ST, tail=False):
     return its
 
 
-def block(ST, P):
+def block(ST, P, HH=True, FF=True):
     out = []          # list of It
     done = set()
 
@@ -158,7 +166,7 @@ def block(ST, P):
         done.discard("F")
         pool = []
         if s > 0:
-            pool += column_items(s - 1, ST)
+            pool += column_items(s - 1, ST, HH, FF)
         pool.append(It("P", f"v_mov_b32_e32 %[{SH(s + 1)}], %[{T(s)}]"))            # lane 0's next shift
         pool += mem.get(s, [])
         chain = []
@@ -187,7 +195,7 @@ def block(ST, P):
             emit(got[0])
     # tail: D and F of column 7, its codes / scores / ring write, then prog
     done.discard("F")
-    pool = column_items(7, ST)
+    pool = column_items(7, ST, HH, FF)
     gap(pool)
     emit(It("D", f"v_mov_b32_dpp %[{SH(8)}], %[{GB(7)}] wave_shr:1 row_mask:0xf bank_mask:0xf"))
     emit(It("F", f"v_max_i32_e32 %[{GA(7)}], %[{XA(7)}], %[{SH(8)}]"))
@@ -195,8 +203,9 @@ def block(ST, P):
         got = take(pool, 1, ())
         assert got, [p.name for p in pool]
         emit(got[0])
-    emit(It("", "v_xor_b32_e32 %[accA], 0xffffff, %[accA]"))                # flags were collected inverted
-    emit(It("", "v_xor_b32_e32 %[accB], 0xffffff, %[accB]"))
+    if FF:
+        emit(It("", "v_xor_b32_e32 %[accA], 0xffffff, %[accA]"))            # flags were collected inverted
+        emit(It("", "v_xor_b32_e32 %[accB], 0xffffff, %[accB]"))
     emit(It("PW", "ds_write_b32 %[cb], %[cv] offset:16", lds=True))         # prog[w+1] = c+1
     lines = [it.text for it in out]
     last = max(i for i, x in enumerate(lines) if x.startswith("ds_read"))
@@ -269,16 +278,16 @@ def main():
     args = ap.parse_args()
     parts = ["// GENERATED by tools/gen_pair_asm.py -- do not edit; see the generator for the schedule.\n",
              OPERANDS,
-             "template <bool ST, bool P>\n"
+             "template <bool HH, bool FF, bool ST, bool P>\n"
              "__device__ __forceinline__ void pair_chunk_asm(PairRegs& r, const PairConst& k, const PairSlot& ts,\n"
              "                                               PairSlot& ns, int cv, int ra, int rd);\n"]
     decl = "    int ga_[7], gb_[7], sh_[8], xa_[2], dga_[2], dgb_[2], t_[8], sp_[4];\n"
     tf = lambda b: "true" if b else "false"
-    for ST in (0, 1):
+    for HH, FF, ST in ((1, 1, 1), (1, 1, 0), (1, 0, 0), (0, 1, 0), (0, 0, 0)):
         for P in (0, 1):
-            lines = block(ST, P)
+            lines = block(ST, P, HH, FF)
             parts.append(
-                f"template <> __device__ __forceinline__ void pair_chunk_asm<{tf(ST)}, {tf(P)}>"
+                f"template <> __device__ __forceinline__ void pair_chunk_asm<{tf(HH)}, {tf(FF)}, {tf(ST)}, {tf(P)}>"
                 f"(PairRegs& r, const PairConst& k, const PairSlot& ts, PairSlot& ns, int cv, int ra, int rd) {{\n"
                 f"{decl}    asm volatile(\n{cstr(lines)}\n"
                 f"        NW_PAIR_OPERANDS : \"vcc\", \"memory\");\n}}\n")
