@@ -112,6 +112,7 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
     __shared__ int scratch[64 + R * SLOT];     // dummy target of the block's ring writes (lanes 0..62)
     __shared__ int sh_sidx;
     __shared__ int sh_abort;
+    __shared__ int sh_done;     // XCD map: this block's one WG-stripe is taken
 
     const int lane = threadIdx.x & 63;
     const int w = uni(threadIdx.x >> 6);
@@ -123,9 +124,16 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
     const int NC = a.NC;
     const int nlast = a.L1 - CH * (NC - 1);   // columns in the last chunk (1..8)
 
+    if (threadIdx.x == 0) sh_done = 0;
     for (;;) {
         if (threadIdx.x == 0) {
-            const int sidx = (int)atomicAdd(&a.ctl[CTL_NEXT], 1u);
+            // XCD map ($NW_XCD): blocks b and b+8 share an XCD (and its L2), so
+            // block b takes WG-stripe (b%8)*q + min(b%8, r) + b/8 (grid = 8q + r):
+            // consecutive WG-stripes hand over inside one L2 except at 7 seams.
+            const int b = blockIdx.x, q = gridDim.x / 8, rr = gridDim.x % 8;
+            const int sidx = a.xcd_map ? (sh_done ? a.NSW : (b % 8) * q + min(b % 8, rr) + b / 8)
+                                       : (int)atomicAdd(&a.ctl[CTL_NEXT], 1u);
+            sh_done = 1;
             sh_sidx = sidx;
             sh_abort = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - (sidx * a.SQ + min(sidx, a.SR)));

@@ -36,6 +36,7 @@ import os
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 OUT = os.path.join(ROOT, "needleman-wunsch_amd", "csrc", "nw_pair_chunk.inc")
+READ_AT = 6            # step whose gaps issue the next slot's progress and data reads
 
 
 def GA(s):
@@ -152,10 +153,13 @@ def block(ST, P, HH=True, FF=True):
     mem = {0: [It("CW", "ds_write_b32 %[cb], %[cv] offset:4", lds=True),            # cons[w] = c+1
                It("W8", "ds_write_b32 %[ra], %[tc0] offset:32", lds=True),          # symbols down the ring
                It("W9", "ds_write_b32 %[ra], %[tc1] offset:36", lds=True)],
-           2: [It("PQ", "ds_read_b64 %[pq], %[cb] offset:8", lds=True)],             # {prog[w], cons[w+1]}
-           3: [It("TA", "ds_read_b128 %[nA], %[rd]", lds=True)],
-           4: [It("TB", "ds_read_b128 %[nB], %[rd] offset:16", lds=True)],
-           5: [It("TC", "ds_read_b64 %[nC], %[rd] offset:32", lds=True)]}
+           # (READ_AT: how late in the block the next slot is read; the
+           # producer runs one chunk ahead, so an early read usually misses it
+           # and the caller takes the slow re-read)
+           READ_AT: [It("PQ", "ds_read_b64 %[pq], %[cb] offset:8", lds=True),       # {prog[w], cons[w+1]}
+                     It("TA", "ds_read_b128 %[nA], %[rd]", lds=True)],
+           READ_AT + 1: [It("TB", "ds_read_b128 %[nB], %[rd] offset:16", lds=True),
+                         It("TC", "ds_read_b64 %[nC], %[rd] offset:32", lds=True)]}
     # head: profile lookups of the chunk, pre-fill of sh_1
     if P:
         out += [It("", "v_perm_b32 %[subA0], %[pha], %[pla], %[tc0]"),
@@ -275,7 +279,9 @@ def cstr(lines):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=OUT)
+    ap.add_argument("--read-at", type=int, default=READ_AT)
     args = ap.parse_args()
+    globals()["READ_AT"] = args.read_at
     parts = ["// GENERATED by tools/gen_pair_asm.py -- do not edit; see the generator for the schedule.\n",
              OPERANDS,
              "template <bool HH, bool FF, bool ST, bool P>\n"
