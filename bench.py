@@ -69,11 +69,22 @@ def cpu_baseline(n):
                              capture_output=True, text=True, timeout=600)
         if out.returncode == 0:
             r = json.loads(out.stdout)
-            return {"value": round(n * n / r["fill_s"] / 1e9, 5), "unit": "GCUPS", "cores": cores,
-                    "kind": "reference",
-                    "sample": f"{n}x{n} random DNA, m=k=d=1: reference compute_table_scores "
-                              f"(needleman-wunsch.c:583, serial, -O3 -DNDEBUG) fill phase "
-                              f"{r['fill_s']:.2f} s, tables calloc'd cold as in the reference"}
+            res = {"value": round(n * n / r["fill_s"] / 1e9, 5), "unit": "GCUPS", "cores": cores,
+                   "kind": "reference",
+                   "sample": f"{n}x{n} random DNA, m=k=d=1: reference compute_table_scores "
+                             f"(needleman-wunsch.c:583, serial, -O3 -DNDEBUG) fill phase "
+                             f"{r['fill_s']:.2f} s, tables calloc'd cold as in the reference"}
+            # The reference's -p path (per-cell mutex/cond hand-off, needleman-wunsch.c:444-475)
+            # on this host's share of cores, on a smaller sample: it is slower than serial.
+            T = min(16, os.cpu_count() or 1)
+            npar = max(256, n // 4)
+            outp = subprocess.run([harness, "gen", str(npar), str(npar), "1", "1", "1", str(T)],
+                                  capture_output=True, text=True, timeout=600)
+            if outp.returncode == 0:
+                rp = json.loads(outp.stdout)
+                res["pthread"] = {"value": round(npar * npar / rp["fill_s"] / 1e9, 5), "unit": "GCUPS",
+                                  "threads": T, "sample": f"{npar}x{npar}, -p {T}: fill phase {rp['fill_s']:.2f} s"}
+            return res
     # Fallback: the clean-room restatement (same algorithm, dense layout).
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O  # checker/baseline only
