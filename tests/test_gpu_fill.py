@@ -196,3 +196,21 @@ def test_100k_config_c3_colchain():
         assert (st2.corner, st2.greatest_abs_interior, st2.branch_count) == \
             (g["corner"], g["gav"], g["branch_count"])
         assert np.array_equal(t.last_column(), last)
+
+
+def test_100k_score_only_last_column_matches_full_fill():
+    """Size-independent check of the score-only path at 100k x 100k: the last
+    column H[L1][*] of a score-only fill (no table stored) equals the last
+    column of the full fill, whose table hashes to the 100k fixture above."""
+    L1 = L2 = 100_000
+    s1, s2 = nw_amd.gen_dna(1, L1), nw_amd.gen_dna(2, L2)
+    SD = nw_amd.NW_OUT_SCORES | nw_amd.NW_OUT_DIRS
+    with nw_amd.Table(L1, L2, SD) as t:
+        t.set_sequences(s1, s2)
+        t.fill(1, 1, 1, SD)
+        full = t.last_column()
+        t.fill(1, 1, 1, 0)
+        so = t.last_column()
+        corner = t.stats().corner
+    assert np.array_equal(full, so)
+    assert corner == full[-1]
