@@ -447,3 +447,110 @@ int64_t nwo_first_path(const uint8_t *D, int64_t L1, int64_t L2, uint8_t *moves)
         }
         return n;
 }
+
+/* ---- score-only band wavefront on T threads (pins the 1M x 1M fill) ---- */
+/* Same recurrence as fill_column (needleman-wunsch.c:429-465) in O(L1 + L2)
+ * memory: thread t owns rows of band t, walks the columns, takes the row
+ * above from band t-1's published bottom row and publishes its own. */
+
+typedef struct {
+        const char *s1, *s2;
+        int64_t L1, L2, nr;       /* rows per band */
+        int32_t m, k, d;
+        int32_t **bnd;            /* bnd[t][i] = H[i][last row of band t] */
+        int64_t *prog;            /* columns of bnd[t] published */
+        int32_t *lastcol;         /* H[L1][0..L2] */
+        int nb;
+} so_ctx;
+
+typedef struct {
+        so_ctx *c;
+        int t;
+} so_arg;
+
+static void *so_worker(void *p)
+{
+        so_arg *a = (so_arg *)p;
+        so_ctx *c = a->c;
+        const int t = a->t;
+        const int64_t r0 = 1 + (int64_t)t * c->nr;
+        const int64_t r1 = (r0 + c->nr - 1 < c->L2) ? r0 + c->nr - 1 : c->L2;
+        const int64_t nr = r1 - r0 + 1;
+        const int32_t m = c->m, k = c->k, d = c->d;
+        int32_t *prev = malloc(sizeof(int32_t) * (size_t)(nr + 1));
+        int32_t *cur = malloc(sizeof(int32_t) * (size_t)(nr + 1));
+        if (!prev || !cur) abort();
+        for (int64_t x = 0; x <= nr; x++) prev[x] = (int32_t)(-(r0 - 1 + x) * (int64_t)d);   /* column 0 */
+        c->bnd[t][0] = prev[nr];
+        int64_t seen = 0;
+        for (int64_t i = 1; i <= c->L1; i++) {
+                int32_t top;
+                if (t == 0) {
+                        top = (int32_t)(-i * (int64_t)d);                   /* row 0 */
+                } else {
+                        while (seen < i) seen = __atomic_load_n(&c->prog[t - 1], __ATOMIC_ACQUIRE);
+                        top = c->bnd[t - 1][i];
+                }
+                cur[0] = top;
+                const char c1 = c->s1[i - 1];
+                const char *s2 = c->s2 + (r0 - 1);
+                for (int64_t x = 1; x <= nr; x++) {
+                        const int32_t dg = prev[x - 1] + (c1 == s2[x - 1] ? m : -k);
+                        const int32_t l = prev[x] - d, u = cur[x - 1] - d;
+                        int32_t v = dg > l ? dg : l;
+                        cur[x] = v > u ? v : u;
+                }
+                c->bnd[t][i] = cur[nr];
+                if ((i & 63) == 0 || i == c->L1) __atomic_store_n(&c->prog[t], i, __ATOMIC_RELEASE);
+                int32_t *tmp = prev;
+                prev = cur;
+                cur = tmp;
+        }
+        memcpy(c->lastcol + r0, prev + 1, sizeof(int32_t) * (size_t)nr);
+        free(prev);
+        free(cur);
+        return NULL;
+}
+
+int32_t nwo_score_only_mt(const char *s1, int64_t L1, const char *s2, int64_t L2,
+                          int32_t m, int32_t k, int32_t d, int nthreads, uint64_t *hlast)
+{
+        if (L1 == 0 || L2 == 0 || nthreads <= 1) return nwo_score_only(s1, L1, s2, L2, m, k, d, hlast);
+        so_ctx c;
+        c.s1 = s1;
+        c.s2 = s2;
+        c.L1 = L1;
+        c.L2 = L2;
+        c.m = m;
+        c.k = k;
+        c.d = d;
+        c.nb = nthreads;
+        c.nr = (L2 + nthreads - 1) / nthreads;
+        while ((c.nb - 1) * c.nr >= L2) c.nb--;      /* no empty bands */
+        c.bnd = malloc(sizeof(int32_t *) * (size_t)c.nb);
+        c.prog = calloc((size_t)c.nb, sizeof(int64_t));
+        c.lastcol = malloc(sizeof(int32_t) * (size_t)(L2 + 1));
+        if (!c.bnd || !c.prog || !c.lastcol) abort();
+        for (int t = 0; t < c.nb; t++) {
+                c.bnd[t] = malloc(sizeof(int32_t) * (size_t)(L1 + 1));
+                if (!c.bnd[t]) abort();
+        }
+        c.lastcol[0] = (int32_t)(-L1 * (int64_t)d);
+        pthread_t *th = malloc(sizeof(pthread_t) * (size_t)c.nb);
+        so_arg *args = malloc(sizeof(so_arg) * (size_t)c.nb);
+        for (int t = 0; t < c.nb; t++) {
+                args[t].c = &c;
+                args[t].t = t;
+                pthread_create(&th[t], NULL, so_worker, &args[t]);
+        }
+        for (int t = 0; t < c.nb; t++) pthread_join(th[t], NULL);
+        if (hlast) *hlast = nwo_fnv1a(NWO_FNV_INIT, c.lastcol, 4 * (L2 + 1));
+        const int32_t r = c.lastcol[L2];
+        for (int t = 0; t < c.nb; t++) free(c.bnd[t]);
+        free(c.bnd);
+        free(c.prog);
+        free(c.lastcol);
+        free(th);
+        free(args);
+        return r;
+}

@@ -64,6 +64,12 @@ int nwo_fill_colchain(const char *s1, int64_t L1, const char *s2, int64_t L2,
 int32_t nwo_score_only(const char *s1, int64_t L1, const char *s2, int64_t L2,
                        int32_t m, int32_t k, int32_t d, uint64_t *hlast);
 
+/* Score-only on nthreads row bands (a band wavefront, O(L1 + L2) memory):
+ * same results as nwo_score_only, for the sizes a single core cannot reach
+ * (the 1M x 1M pin, tests/golden/make_big_scoreonly.py). */
+int32_t nwo_score_only_mt(const char *s1, int64_t L1, const char *s2, int64_t L2,
+                          int32_t m, int32_t k, int32_t d, int nthreads, uint64_t *hlast);
+
 /* Blocked anti-diagonal multi-threaded full fill (CPU baseline, same output
  * as nwo_fill; D may be NULL, stats may be NULL). */
 int nwo_fill_mt(const char *s1, int64_t L1, const char *s2, int64_t L2,

@@ -39,6 +39,9 @@ def lib():
         L.nwo_score_only.restype = ctypes.c_int32
         L.nwo_score_only.argtypes = [ctypes.c_char_p, i64, ctypes.c_char_p, i64, i32, i32, i32,
                                      ctypes.POINTER(ctypes.c_uint64)]
+        L.nwo_score_only_mt.restype = ctypes.c_int32
+        L.nwo_score_only_mt.argtypes = [ctypes.c_char_p, i64, ctypes.c_char_p, i64, i32, i32, i32, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_uint64)]
         L.nwo_fill_mt.argtypes = [ctypes.c_char_p, i64, ctypes.c_char_p, i64, i32, i32, i32, p, p,
                                   ctypes.POINTER(Stats), ctypes.c_int]
         L.nwo_gen_dna.argtypes = [ctypes.c_uint64, i64, ctypes.c_char_p]
@@ -99,6 +102,19 @@ def score_only(s1, s2, m, k, d):
     h = ctypes.c_uint64()
     c = lib().nwo_score_only(s1, len(s1), s2, len(s2), m, k, d, ctypes.byref(h))
     return c, h.value
+
+
+def score_only_mt(s1, s2, m, k, d, threads):
+    """score_only on `threads` row bands: (corner, FNV of the last column)."""
+    h = ctypes.c_uint64()
+    c = lib().nwo_score_only_mt(s1, len(s1), s2, len(s2), m, k, d, threads, ctypes.byref(h))
+    return c, h.value
+
+
+def fnv_bytes(buf) -> int:
+    """FNV-1a-64 of a bytes-like buffer (the oracle's nwo_fnv1a)."""
+    b = bytes(buf)
+    return lib().nwo_fnv1a(0xCBF29CE484222325, b, len(b))
 
 
 def kat_inputs(case):

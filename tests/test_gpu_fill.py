@@ -214,3 +214,17 @@ def test_100k_score_only_last_column_matches_full_fill():
         corner = t.stats().corner
     assert np.array_equal(full, so)
     assert corner == full[-1]
+
+
+def test_1m_score_only_pinned():
+    """configs[4]: 1M x 1M score-only (no table; 4 TB would not fit).  Corner
+    and the FNV of the last row H[L1][0..L2] against tests/golden/big_scoreonly.json,
+    written by the oracle's multithreaded restatement (make_big_scoreonly.py)."""
+    from conftest import load_golden
+    g = load_golden("big_scoreonly.json")[0]
+    s1, s2 = nw_amd.gen_dna(1, g["L1"]), nw_amd.gen_dna(2, g["L2"])
+    with nw_amd.Table(g["L1"], g["L2"], nw_amd.NW_OUT_STATS) as t:
+        t.set_sequences(s1, s2)
+        t.fill(g["m"], g["k"], g["d"], nw_amd.NW_OUT_STATS)
+        assert t.stats().corner == g["corner"]
+        assert "%016x" % O.fnv(t.last_column()) == g["lastcol_fnv"]
