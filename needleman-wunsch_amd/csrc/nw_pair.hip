@@ -218,6 +218,8 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
             };
             int cw = 0;
             uint64_t pf = 0, pn = 0;
+            PollRegs pq4;                      // poll_window's loads still in flight
+            bool polled = false;
             uint32_t pc = chl ? s1w[lane - 8] : 0u;
             if (!seeded) {
                 pf = gload(0);
@@ -242,8 +244,15 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                     if (!__all(ok)) {
                         const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
                         for (;;) {
-                            __builtin_amdgcn_s_sleep(1);
-                            if (wk >= c - cw && (uint32_t)(pf >> 32) != want) pf = gload(cw);
+                            if (NW_POLL_ASM && !xsrc) {
+                                // NW_POLL_ASM (nw_kern.h poll_window): 4 staggered polls in flight
+                                const uint64_t* pa = gin + min((int64_t)CH * cw + lane, ngr - 1);
+                                poll_window(pf, pa, want, __ballot(mine && wb < n), __ballot(wk >= c - cw), pq4);
+                                polled = true;
+                            } else {
+                                __builtin_amdgcn_s_sleep(1);
+                                if (wk >= c - cw && (uint32_t)(pf >> 32) != want) pf = gload(cw);
+                            }
                             ok = !mine || wb >= n || (uint32_t)(pf >> 32) == want;
                             if (__all(ok)) break;
                             const int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
@@ -274,6 +283,9 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                 lds_order();
                 if (lane == 0) lds_publish(&ctr[2], c + 1);
             }
+            // poll_window's last loads land in pq4 (a new poll reuses the same
+            // registers: in-order returns make that safe, so only the exit drains)
+            if (polled) poll_drain(pq4);
         } else if (real) {
             // ---------------- compute wave: its 128-row stripe, chunk by chunk ----
             // virtual 64-row stripes 2g (rows a) and 2g+1 (rows b): a.spitch = 1024*NC
