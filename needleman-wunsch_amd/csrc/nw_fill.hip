@@ -166,11 +166,7 @@ __device__ __forceinline__ void store_chunk_scores(const ChunkRegs& r, const Chu
         qa = v4i{r.g[0] + nl + k.kd[0], r.g[1] + nl + k.kd[1], r.g[2] + nl + k.kd[2], r.g[3] + nl + k.kd[3]};
         qb = v4i{r.g[4] + nl + k.kd[4], r.g[5] + nl + k.kd[5], r.gp6 + nl + k.kd[6], r.gin + nl + k.kd[7]};
     }
-#ifdef NW_DIAG_FIXED_SCORES
-    const int hv = (int)(threadIdx.x & 63) * 16;   // diagnostic: no score traffic beyond one line per lane
-#else
     const int hv = r.hv;
-#endif
     asm volatile(
         "global_store_dwordx4 %[hv], %[qa], %[hb]" NW_SCORE_HINT "\n\t"
         "global_store_dwordx4 %[hv], %[qb], %[hb] offset:1024" NW_SCORE_HINT
@@ -210,7 +206,6 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
     __shared__ __attribute__((aligned(8))) int ctr[2 * W + 4];
     __shared__ int sh_sidx;
     __shared__ int sh_abort;
-    __shared__ int sh_done;     // XCD map: this block's one WG-stripe is taken
 
     const int lane = threadIdx.x & 63;
     const int w = uni(threadIdx.x >> 6);
@@ -221,19 +216,10 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
     int vck = 2 * a.d - a.k;
     const int NC = a.NC;
     const int nlast = a.L1 - CH * (NC - 1);   // steps in the last chunk (1..8)
-    if (threadIdx.x == 0) sh_done = 0;
 
     for (;;) {
         if (threadIdx.x == 0) {
-            // XCD map: blocks b and b+8 share an XCD (and its L2), so block
-            // b takes WG-stripe (b%8)*q + min(b%8, r) + b/8 (grid = 8q + r):
-            // the hand-offs between consecutive WG-stripes stay inside one
-            // L2 except at 7 group boundaries.  Every block holds exactly
-            // one WG-stripe and waits only on a block that holds another.
-            const int b = blockIdx.x, q = gridDim.x / 8, rr = gridDim.x % 8;
-            const int sidx = a.xcd_map ? (sh_done ? a.NSW : (b % 8) * q + min(b % 8, rr) + b / 8)
-                                       : (int)atomicAdd(&a.ctl[CTL_NEXT], 1u);
-            sh_done = 1;
+            const int sidx = (int)atomicAdd(&a.ctl[CTL_NEXT], 1u);
             sh_sidx = sidx;
             sh_abort = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - (sidx * a.SQ + min(sidx, a.SR)));
@@ -899,13 +885,6 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         // and of the transport (RCCL), which its hand-off waits on.
         const int per_cu = panel ? std::max(1, std::min(2, occ - 1)) : std::min(occ, 16);
         const int64_t grid = std::min<int64_t>(a.NSW, (int64_t)t->ncu * per_cu);
-        // One WG-stripe per block when the grid covers them all (a plain fill
-        // with all blocks resident); panels keep the dequeue (their
-        // neighbours' kernels share the CUs).
-        {
-            const char* e = getenv("NW_XCD");
-            a.xcd_map = (!skew && !panel && grid == a.NSW && (e ? atoi(e) != 0 : NW_XCD_DEFAULT)) ? 1 : 0;
-        }
         a.nslot = (int32_t)std::min<int64_t>(grid + 1, (int64_t)(t->gran_bytes / 8 / a.gpitch));
         if (a.nslot < grid + 1) return fail(NW_ERR_ARG, "nw_table_fill: granule buffer too small");
         if (a.NSW > 1) NW_HIPCHK(hipMemsetAsync(t->gran, 0, (size_t)a.nslot * a.gpitch * 8, t->stream));

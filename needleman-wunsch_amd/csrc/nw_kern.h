@@ -11,20 +11,6 @@
 namespace nwk {
 
 constexpr int CH = 8;                 // columns per chunk (= codes per dirs word)
-#ifndef NW_XCD_DEFAULT
-#define NW_XCD_DEFAULT 0
-#endif
-// Pair loader: poll the hand-off granules with poll_window (4 staggered loads
-// in flight) instead of one load at a time; NW_POLL_GAP = their initial
-// spacing in s_sleep units (64 cycles).
-#ifndef NW_POLL_ASM
-#define NW_POLL_ASM 0
-#endif
-#ifndef NW_POLL_GAP
-#define NW_POLL_GAP 6
-#endif
-#define NW_STR2(x) #x
-#define NW_STR(x) NW_STR2(x)
 constexpr int64_t SPIN_TICKS = 200000000;  // 2 s of s_memrealtime (100 MHz)
 // Panel boundary granule tags: the fill's epoch (1 .. 2^31-1), or the epoch
 // with bit 31 set when the panel above failed that fill (per-epoch, so a stale
@@ -62,7 +48,6 @@ struct FillArgs {
     uint64_t* xout;         // bottom row granules for the panel below, or null
     uint32_t* xflag;        // host-visible: xflag[b] = epoch once block b of xout is written
     int32_t xblk;           // chunks per block
-    int32_t xcd_map;        // 1: one WG-stripe per block, consecutive WG-stripes on blocks of one XCD
 };
 
 // ---------------------------------------------------------------- DPP helpers
@@ -92,72 +77,6 @@ constexpr int SLOT = 16;
 __device__ __forceinline__ uint64_t ld_gran(const uint64_t* p, bool sys) {
     return sys ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Pipelined granule poll (loader wave, NW_POLL_ASM).  An sc1 round trip is
-// 2-3 us once the consumer CU's memory queue carries table stores, so one
-// load at a time sees a granule ~1.5 round trips after it lands on average.
-// poll_window keeps 4 loads of the window in flight, issued ~64*NW_POLL_GAP
-// cycles apart, and each check waits only for the oldest (vmcnt(3)): ~1 round
-// trip.  A check merges the poll into pf on the `refresh` lanes whose tag is
-// not `want` yet and returns once every `need` lane's tag is `want`, or after
-// 64 rounds (the caller then checks abort / timeout and calls again).  The
-// compiler's own waits cannot express this (it drains to vmcnt(0) or rotates
-// the reloads through one register), hence one asm block with 64-bit
-// operands only.  On return up to 3 loads are still in flight into r: keep r
-// alive and call poll_drain before it goes out of scope or is reused (after
-// the ring write is published, off the hand-off path).  pa: this lane's
-// granule (in bounds); EXEC full.
-struct PollRegs {
-    uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
-};
-
-#define NW_POLL_STEP(Q)                                                      \
-    "s_waitcnt vmcnt(3)\n\t"                                                 \
-    "v_lshrrev_b64 %[t], 32, %[pf]\n\t"                                      \
-    "v_cmp_ne_u64_e64 %[m], %[t], %[w]\n\t"                                  \
-    "s_and_b64 %[m], %[m], %[rf]\n\t"                                        \
-    "s_and_saveexec_b64 %[sv], %[m]\n\t"                                     \
-    "v_pk_mov_b32 %[pf], %[" Q "], %[" Q "] op_sel:[0,1]\n\t"                \
-    "s_mov_b64 exec, %[sv]\n\t"                                              \
-    "v_lshrrev_b64 %[t], 32, %[pf]\n\t"                                      \
-    "v_cmp_ne_u64_e64 %[m], %[t], %[w]\n\t"                                  \
-    "s_and_b64 %[m], %[m], %[need]\n\t"                                      \
-    "s_cmp_eq_u64 %[m], 0\n\t"                                               \
-    "s_cbranch_scc1 2f\n\t"                                                  \
-    "s_sleep 1\n\t"                                                          \
-    "global_load_dwordx2 %[" Q "], %[pa], off sc1\n\t"
-
-__device__ __forceinline__ void poll_window(uint64_t& pf, const uint64_t* pa, uint32_t want, uint64_t need,
-                                            uint64_t refresh, PollRegs& r) {
-    const uint64_t want64 = want;
-    uint64_t m, sv, t;
-    uint32_t cnt;
-    asm volatile(
-        "global_load_dwordx2 %[q0], %[pa], off sc1\n\t"
-        "s_sleep " NW_STR(NW_POLL_GAP) "\n\t"
-        "global_load_dwordx2 %[q1], %[pa], off sc1\n\t"
-        "s_sleep " NW_STR(NW_POLL_GAP) "\n\t"
-        "global_load_dwordx2 %[q2], %[pa], off sc1\n\t"
-        "s_sleep " NW_STR(NW_POLL_GAP) "\n\t"
-        "global_load_dwordx2 %[q3], %[pa], off sc1\n\t"
-        "s_mov_b32 %[cnt], 64\n"
-        "1:\n\t"
-        NW_POLL_STEP("q0") NW_POLL_STEP("q1") NW_POLL_STEP("q2") NW_POLL_STEP("q3")
-        "s_sub_u32 %[cnt], %[cnt], 1\n\t"
-        "s_cmp_lg_u32 %[cnt], 0\n\t"
-        "s_cbranch_scc1 1b\n"
-        "2:\n\t"
-        : [pf] "+v"(pf), [q0] "+v"(r.q0), [q1] "+v"(r.q1), [q2] "+v"(r.q2), [q3] "+v"(r.q3), [m] "=&s"(m),
-          [sv] "=&s"(sv), [t] "=&v"(t), [cnt] "=&s"(cnt)
-        : [pa] "v"(pa), [w] "s"(want64), [need] "s"(need), [rf] "s"(refresh)
-        : "scc", "memory");
-}
-#undef NW_POLL_STEP
-
-// Wait for poll_window's loads still in flight (their registers stay live up to here).
-__device__ __forceinline__ void poll_drain(PollRegs& r) {
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(r.q0), "+v"(r.q1), "+v"(r.q2), "+v"(r.q3)::"memory");
 }
 
 // LDS counters of the barrier-free intra-workgroup pipeline.

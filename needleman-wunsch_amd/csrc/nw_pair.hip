@@ -112,7 +112,6 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
     __shared__ int scratch[64 + R * SLOT];     // dummy target of the block's ring writes (lanes 0..62)
     __shared__ int sh_sidx;
     __shared__ int sh_abort;
-    __shared__ int sh_done;     // XCD map: this block's one WG-stripe is taken
 
     const int lane = threadIdx.x & 63;
     const int w = uni(threadIdx.x >> 6);
@@ -124,16 +123,9 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
     const int NC = a.NC;
     const int nlast = a.L1 - CH * (NC - 1);   // columns in the last chunk (1..8)
 
-    if (threadIdx.x == 0) sh_done = 0;
     for (;;) {
         if (threadIdx.x == 0) {
-            // XCD map ($NW_XCD): blocks b and b+8 share an XCD (and its L2), so
-            // block b takes WG-stripe (b%8)*q + min(b%8, r) + b/8 (grid = 8q + r):
-            // consecutive WG-stripes hand over inside one L2 except at 7 seams.
-            const int b = blockIdx.x, q = gridDim.x / 8, rr = gridDim.x % 8;
-            const int sidx = a.xcd_map ? (sh_done ? a.NSW : (b % 8) * q + min(b % 8, rr) + b / 8)
-                                       : (int)atomicAdd(&a.ctl[CTL_NEXT], 1u);
-            sh_done = 1;
+            const int sidx = (int)atomicAdd(&a.ctl[CTL_NEXT], 1u);
             sh_sidx = sidx;
             sh_abort = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - (sidx * a.SQ + min(sidx, a.SR)));
@@ -218,8 +210,6 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
             };
             int cw = 0;
             uint64_t pf = 0, pn = 0;
-            PollRegs pq4;                      // poll_window's loads still in flight
-            bool polled = false;
             uint32_t pc = chl ? s1w[lane - 8] : 0u;
             if (!seeded) {
                 pf = gload(0);
@@ -244,15 +234,8 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                     if (!__all(ok)) {
                         const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
                         for (;;) {
-                            if (NW_POLL_ASM && !xsrc) {
-                                // NW_POLL_ASM (nw_kern.h poll_window): 4 staggered polls in flight
-                                const uint64_t* pa = gin + min((int64_t)CH * cw + lane, ngr - 1);
-                                poll_window(pf, pa, want, __ballot(mine && wb < n), __ballot(wk >= c - cw), pq4);
-                                polled = true;
-                            } else {
-                                __builtin_amdgcn_s_sleep(1);
-                                if (wk >= c - cw && (uint32_t)(pf >> 32) != want) pf = gload(cw);
-                            }
+                            __builtin_amdgcn_s_sleep(1);
+                            if (wk >= c - cw && (uint32_t)(pf >> 32) != want) pf = gload(cw);
                             ok = !mine || wb >= n || (uint32_t)(pf >> 32) == want;
                             if (__all(ok)) break;
                             const int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
@@ -283,9 +266,6 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                 lds_order();
                 if (lane == 0) lds_publish(&ctr[2], c + 1);
             }
-            // poll_window's last loads land in pq4 (a new poll reuses the same
-            // registers: in-order returns make that safe, so only the exit drains)
-            if (polled) poll_drain(pq4);
         } else if (real) {
             // ---------------- compute wave: its 128-row stripe, chunk by chunk ----
             // virtual 64-row stripes 2g (rows a) and 2g+1 (rows b): a.spitch = 1024*NC

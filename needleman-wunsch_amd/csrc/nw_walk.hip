@@ -254,8 +254,12 @@ int nw_table_count_alignments(nw_table* t, uint32_t* count) {
     int rc = check_walkable(t, "nw_table_count_alignments");
     if (rc) return rc;
     if (!count) return nwi::fail(NW_ERR_ARG, "nw_table_count_alignments: NULL count");
-    if (t->L1 == 0 || t->L2 == 0) {   // one path along the seeded row or column
-        *count = 1;
+    if (t->L1 == 0 || t->L2 == 0) {
+        // One path along the seeded row or column -- or none for two empty
+        // strings: the walk starts on (0,0), whose three directions are
+        // already done (computation.c:96-99), so the loop never runs and no
+        // solution is counted (needleman-wunsch.c:231-235).
+        *count = (t->L1 == 0 && t->L2 == 0) ? 0u : 1u;
         return NW_OK;
     }
     NW_HIPCHK(hipSetDevice(t->device));

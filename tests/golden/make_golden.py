@@ -101,6 +101,15 @@ CLI_CASES = [
     ("many_alignments", ["-s", "-l", "1", "1", "1"], "AAAA AA\n"),
     ("empty_s1", ["-s", "-t", "1", "1", "1"], "   ACGT\n"),
     ("empty_s1_s2", ["-s", "-t", "1", "1", "1"], "\n\n  \n"),
+    ("empty_s1_s2_q_s", ["-q", "-s", "1", "1", "1"], "\n\n  \n"),
+    ("nul_token_q_s", ["-q", "-s", "1", "1", "1"], " \0"),
+    ("empty_s1_q_s", ["-q", "-s", "1", "1", "1"], "   ACGT\n"),
+    # many co-optimal alignments: the enumeration order (diag > left > up)
+    ("many_alignments_924_l", ["-l", "-s", "1", "1", "1"], "AAAAAAAAAAAA AAAAAA\n"),
+    ("many_alignments_252", ["1", "1", "1"], "AAAAAAAAAA AAAAA\n"),
+    ("many_alignments_ql_t", ["-q", "-l", "-t", "1", "1", "1"], "ACACACACAC CACACA\n"),
+    ("random_48_ql", ["-q", "-l", "-s", "--", "1", "1", "1"],
+     "GGTCCTTGCTCGAACGTGCAGATACAGTTAGCCATTGACCGATTGCAA GGGTCCGGCGCCTATTCAGACGGAACCTGTTACCAGGATTACGCATT\n"),
     ("third_token_ignored", ["-s", "-l", "1", "1", "1"], "ACGT AGT CCCC\n"),
     ("multiline", ["-s", "1", "1", "1"], "ACGTTGCA\n\n\tAGTTCA"),
     ("threads_p2", ["-p", "2", "-s", "-t", "1", "1", "1"], "GCATGCU GATTACA\n"),

@@ -83,7 +83,8 @@ def read_two(text):
     j = i
     while j < len(b) and b[j] not in ws:
         j += 1
-    return s1, b[i:j]
+    # the reference handles the tokens as C strings (strlen, computation.c:158-160)
+    return s1.split(b"\0")[0], b[i:j].split(b"\0")[0]
 
 
 def render(case):
