@@ -3,7 +3,8 @@
 Launched by the driver as
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
-one process per GPU (LOCAL_RANK = device).  Each rank fills its row panel
+or started by a plain `python bench.py --gpus N` (bench.spawn_ranks), one
+process per GPU (LOCAL_RANK = device).  Each rank fills its row panel
 (include/nw_panel.h) of the SAME table; the panels hand their bottom row down
 the chain as the fill runs.  `value` = L1*L2 / (max over ranks of the time of
 one whole fill), i.e. strong scaling of one table.
@@ -129,14 +130,13 @@ def main(a) -> None:
         slow = max(info, key=lambda r: r["kernel_ms"])
         alg = bpc * (L1 + 1) * (slow["rows"] + 1)
         achieved = alg / (slow["kernel_ms"] * 1e-3) / 1e9 if slow["kernel_ms"] > 0 else 0.0
+        import bench
         out = {
-            "metric": "GCUPS (cell updates/s), 100k x 100k NW score-table fill",
+            "metric": bench.metric_name(L1, L2),
             "value": round(value, 2), "unit": "GCUPS", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "int32", "data": "synthetic (splitmix64 DNA, seeds 1/2)",
-            "config": {"workload": f"{L1}x{L2} " + ("full-table fill (scores+direction codes)"
-                                                     if a.outputs == "sd" else f"fill writing '{a.outputs}'")
-                                   + f", m,k,d={m},{k},{d}",
+            "config": {"workload": bench.workload_name(L1, L2, a.outputs, (m, k, d)),
                        "L1": L1, "L2": L2, "parallelism": f"row panels x{world} ({transport})",
                        "corner": st.corner, "status": rc,
                        "panels": [{"rank": r["rank"], "rows": r["rows"], "kernel_ms": round(r["kernel_ms"], 4),
@@ -145,6 +145,7 @@ def main(a) -> None:
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "bytes_per_cell": bpc, "traffic": None,
                          "kernel_ms": round(slow["kernel_ms"], 4), "alg_bytes_per_launch": alg,
                          "kernel_rank": slow["rank"]},
+            "parity": dict(bench.parity(L1, L2, (m, k, d), {"corner": st.corner}), status=rc),
             "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)

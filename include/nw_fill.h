@@ -130,6 +130,15 @@ int nw_table_elapsed_ms(nw_table *t, float *fill_kernel_ms, float *fill_call_ms)
  * column's int32 LE scores, i = 0..L1; hD likewise over one code byte per
  * cell.  Computed on the device. */
 int nw_table_hash(nw_table *t, uint64_t *hH, uint64_t *hD);
+/* The same hashes, split by rows: continue the per-column FNV-1a-64 states
+ * hstate / dstate (host, L1+1 each, in place) over rows j0..L2 of this table.
+ * A whole table: states = 0xcbf29ce484222325, j0 = 0.  Row panels
+ * (nw_panel.h) chain them panel by panel (the first panel from j0 = 0, every
+ * later one from its first own row, j0 = 1); nw_hash_fold() of the final
+ * states is nw_table_hash()'s hH / hD of the whole table. */
+int nw_table_hash_columns(nw_table *t, int64_t j0, uint64_t *hstate, uint64_t *dstate);
+/* FNV-1a-64 over the 8-byte LE words state[0..n). */
+uint64_t nw_hash_fold(const uint64_t *state, int64_t n);
 /* Copy columns [i0, i1) of the score table to host, dense ((i1-i0)*(L2+1)). */
 int nw_table_copy_scores(nw_table *t, int64_t i0, int64_t i1, int32_t *dst);
 /* Copy the direction codes of columns [i0, i1) to host, one byte per cell. */

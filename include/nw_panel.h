@@ -5,7 +5,8 @@
  * :557-574, :583-626), where thread t owns columns t+1, t+1+T, ... and waits
  * per cell for its left neighbour.  Across GPUs the table is split instead into
  * contiguous ROW panels: panel r holds global rows row_base+1 .. row_base+rows
- * (whole 64-row stripes; every panel but the last has a multiple of 64 rows)
+ * (whole 128-row stripes; every panel but the last has a multiple of 128 rows,
+ * so every feeding panel can run the two-rows-per-lane kernel)
  * for all columns.  This is SURVEY.md section 8(e)'s column-panel scheme
  * transposed to this fill's stripe orientation (waves sweep columns): the
  * exchange is the single boundary ROW, in blocks of columns, and a panel
@@ -23,6 +24,20 @@
  *     Two communicators, so a rank's send and receive links never share one.
  * A failed panel poisons the row it owes (tag = epoch | 2^31) so the panels
  * below stop with NW_ERR_PEER instead of waiting for the watchdog.
+ *
+ * Back-pressure (GROUP / IPC): ranks call nw_panel_fill with no barrier, so a
+ * producer may start fill E+1 while the panel below still reads fill E's row.
+ * The consumer's loader copies the row above into its own table (row0) as it
+ * reads it, then posts E into a credit word behind its boundary buffer; the
+ * producer's first boundary store of fill E+1 waits (in its kernel) until that
+ * word reads E.  Every panel posts for every fill, so the chain never waits on
+ * a panel with nothing to read.  RCCL needs no credit: a send completes only
+ * into a posted receive, and receives are posted per fill.
+ *
+ * RCCL transport: EXPERIMENTAL.  It relies on RCCL's copy kernels writing
+ * each aligned 8-byte {epoch, value} granule untorn (they move >= 16-byte
+ * aligned vectors), which the consumer's tag poll assumes; it has not been
+ * run on more than one GPU (RCCL refuses two ranks on one device).
  *
  * Stats of the whole table are bit-identical to a single-GPU fill: corner
  * from the last panel, max of greatest_abs_interior, sum of branch_count.  The local rows stay device-resident in the panel's
@@ -54,7 +69,7 @@ enum nw_panel_transport {
 #define NW_PANEL_IPC_BYTES 64   /* hipIpcMemHandle_t of a boundary buffer      */
 #define NW_PANEL_REC       8    /* int64 words of one rank's stats record      */
 
-/* Row split of an L2-row table over nranks panels: whole 64-row stripes,
+/* Row split of an L2-row table over nranks panels: whole 128-row stripes,
  * balanced to within one stripe.  Pure host logic (no device needed). */
 int nw_panel_partition(int64_t L2, int nranks, int rank, int64_t *row_base, int64_t *rows);
 
@@ -100,6 +115,13 @@ int nw_panel_group_fill(nw_panel *const *ps, int n, int32_t m, int32_t k, int32_
 int nw_panel_stats(nw_panel *p, nw_stats *st);
 int nw_panel_record(nw_panel *p, int64_t rec[NW_PANEL_REC]);
 int nw_panel_reduce(const int64_t *recs, int nranks, nw_stats *st);   /* pure; first error wins */
+
+/* Whole-table parity hashes across panels: continue the per-column FNV
+ * states (host, L1+1 each, in place; start at 0xcbf29ce484222325) over this
+ * panel's own rows.  Called on every panel in rank order (any transport; the
+ * states travel with the caller), nw_hash_fold() of the result is the
+ * single-GPU nw_table_hash(). */
+int nw_panel_hash_columns(nw_panel *p, uint64_t *hstate, uint64_t *dstate);
 
 /* This panel's rows and its device-resident table (owned by the panel). */
 int nw_panel_rows(const nw_panel *p, int64_t *row_base, int64_t *rows);

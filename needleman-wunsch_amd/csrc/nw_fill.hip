@@ -258,6 +258,10 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
             uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
             const int* bot = &tring[nw * R * SLOT];
             int cd = 0;
+            if (xpublish && !xcredit_wait(a, &sh_abort)) {
+                if (lane == 0) __hip_atomic_store(&sh_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                cd = NC;
+            }
             while ((publish || xpublish) && cd < NC) {
                 const int p = uni(lds_ld(&ctr[2 * nw + 2]));          // prog of the last wave's ring
                 if (p <= cd) {
@@ -364,6 +368,7 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
                     if (lds_ld(&sh_abort)) break;
                     // H - d of the row above -> G' of lane -1: + (i - base)*d
                     if (mine) dst[wb] = (int)(uint32_t)pf + (CH * c + wb + 1 - base) * d;
+                    if (xsrc && mine && wb < n) a.row0[CH * c + wb] = (int)(uint32_t)pf;
                 }
                 if (chl) {
                     dst[lane] = (int)pc;
@@ -371,6 +376,7 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
                 }
                 if (lane == 0) lds_publish(&ctr[2], c + 1);
             }
+            if (xsrc) xcredit_post(a);
         } else if (real) {
             // ---------------- compute wave: its 64-row stripe, chunk by chunk ----
             int32_t* tile = a.H + (int64_t)g * a.spitch;
@@ -576,12 +582,12 @@ struct TableView {
     int32_t pair;           // 1: column layout with rows permuted (nw_pair.hip)
     int32_t d;
     int32_t row_base;       // panels: global row of local row 0
-    const uint64_t* top;    // panels: boundary row granules (H - d), or null for row 0 = seed
+    const int32_t* top;     // panels: the row above (H - d, nw_table.row0), or null for row 0 = seed
 };
 
 // Score of cell (i, j) in the device layout.  Row 0 and column 0 are the
 // reference's seeds (computation.c:93-120), computed, not stored; a panel's
-// row 0 is the last row of the panel above, kept in its xin granules.
+// row 0 is the last row of the panel above, kept in row0 by the loader.
 // Interior cells live in stripe tiles: stripe g = (j-1)/64, lane l =
 // (j-1)%64, spitch = 512*NC elements per stripe.  Quad tiles (NW_SCORE_X4):
 // column i = 4q + r + 1 at g*spitch + (q*64 + l)*4 + r, so a lane's 4
@@ -614,7 +620,7 @@ __host__ __device__ __forceinline__ int64_t code_word(int64_t i, int64_t j, int6
 
 __device__ __forceinline__ int32_t score_at(const TableView& v, int64_t i, int64_t j) {
     if (i == 0) return (int32_t)(-(j + v.row_base) * (int64_t)v.d);
-    if (j == 0) return v.top ? (int32_t)(uint32_t)v.top[i - 1] + v.d : (int32_t)(-i * (int64_t)v.d);
+    if (j == 0) return v.top ? v.top[i - 1] + v.d : (int32_t)(-i * (int64_t)v.d);
     return v.tiles[score_index(j - 1, i - 1, v.spitch, v.skew, v.pair)];
 }
 
@@ -661,13 +667,16 @@ __global__ void nw_codes_kernel(TableView v, int32_t L2, int64_t i0, int64_t i1,
         out[x] = (uint8_t)code_at(v, i0 + x / N, x % N);
 }
 
-// Per-column FNV-1a-64 of scores (int32 LE bytes) and codes (1 byte/cell).
-__global__ void nw_colhash_kernel(TableView v, int32_t L1, int32_t L2, uint64_t* hcol, uint64_t* dcol) {
+// Per-column FNV-1a-64 of scores (int32 LE bytes) and codes (1 byte/cell)
+// over rows j0..L2, continuing from the states in hcol / dcol (in place).  A
+// whole table starts every column at the FNV offset basis with j0 = 0; a row
+// panel continues the panel above's states from its first own row (j0 = 1).
+__global__ void nw_colhash_kernel(TableView v, int32_t L1, int32_t L2, int32_t j0, uint64_t* hcol, uint64_t* dcol) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i > L1) return;
     const uint64_t P = 0x100000001b3ULL;
-    uint64_t h = 0xcbf29ce484222325ULL, e = 0xcbf29ce484222325ULL;
-    for (int64_t j = 0; j <= L2; ++j) {
+    uint64_t h = hcol[i], e = dcol[i];
+    for (int64_t j = j0; j <= L2; ++j) {
         const uint32_t x = (uint32_t)score_at(v, i, j);
         h = (h ^ (x & 0xff)) * P;
         h = (h ^ ((x >> 8) & 0xff)) * P;
@@ -750,7 +759,7 @@ TableView view_of(const nw_table* t) {
     v.pair = t->pair;
     v.d = t->last_d;
     v.row_base = (int32_t)t->row_base;
-    v.top = t->row_base > 0 ? t->xin : nullptr;
+    v.top = t->row_base > 0 ? t->row0 : nullptr;
     return v;
 }
 
@@ -857,13 +866,17 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         a.ctl = t->ctl;
         // A panel waits on another GPU (or process) that may start seconds
         // later; a plain fill only on itself.
-        a.spin_ticks = t->xin ? 30 * SPIN_TICKS : SPIN_TICKS;
+        a.spin_ticks = (t->xin || t->xout) ? 30 * SPIN_TICKS : SPIN_TICKS;
         a.row_base = (int32_t)t->row_base;
         a.epoch = t->epoch;
         a.xin = t->xin;
         a.xout = t->xout;
         a.xflag = t->xflag;
         a.xblk = (int32_t)std::max<int64_t>(t->xblk, 1);
+        a.row0 = t->row0;
+        a.xin_credit = t->xin ? t->xin_credit : nullptr;
+        a.xout_credit = t->xout ? t->xout_credit : nullptr;
+        a.credit_want = t->credit_want;
         if (t->xout && (L2 % 64) != 0) return fail(NW_ERR_ARG, "nw_table_fill: a feeding panel needs 64*k rows");
         if (getenv("NW_TRACE")) {
             const int64_t need = 8 * (int64_t)a.NSW;
@@ -896,6 +909,8 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         NW_HIPCHK(hipEventRecord(t->ev[2], t->stream));
     } else {
         NW_HIPCHK(hipEventRecord(t->ev[1], t->stream));
+        // no kernel reads the row above: release it for the producer's next fill
+        if (t->xin && t->xin_credit) NW_HIPCHK(hipMemsetD32Async(t->xin_credit, (int)t->epoch, 1, t->stream));
         NW_HIPCHK(hipEventRecord(t->ev[2], t->stream));
     }
     t->launched = true;
@@ -985,6 +1000,7 @@ void nw_table_destroy(nw_table* t) {
     (void)hipFree(t->H);
     (void)hipFree(t->D);
     (void)hipFree(t->lastcol);
+    (void)hipFree(t->row0);
     (void)hipFree(t->gran);
     (void)hipFree(t->ctl);
     (void)hipFree(t->trace);
@@ -1046,6 +1062,7 @@ int nw_table_create(int device, int64_t max_L1, int64_t max_L2, uint32_t out_mas
         if ((rc = alloc((void**)&t->D, (size_t)(NG + 1) * (NC + 9) * 256))) return bail(rc);
     }
     if ((rc = alloc((void**)&t->lastcol, (size_t)(64 * NG + 128) * 4))) return bail(rc);
+    if ((rc = alloc((void**)&t->row0, (size_t)(max_L1 + 8) * 4))) return bail(rc);
     // Granule slots: one per concurrently running WG-stripe + 1.
     const int64_t gpitch = CH * NC + CH;
     const int64_t nslot = 16 * (int64_t)t->ncu + 1;
@@ -1175,10 +1192,10 @@ int nw_table_copy_last_column(nw_table* t, int32_t* dst) {
     }
     // Row 0: the seed, or (panels) the last row of the panel above.
     if (t->row_base > 0) {
-        uint64_t g = 0;
-        HIPCHK(hipMemcpyAsync(&g, t->xin + (t->L1 - 1), 8, hipMemcpyDeviceToHost, t->stream));
+        int32_t g = 0;
+        HIPCHK(hipMemcpyAsync(&g, t->row0 + (t->L1 - 1), 4, hipMemcpyDeviceToHost, t->stream));
         HIPCHK(hipStreamSynchronize(t->stream));
-        dst[0] = (int32_t)(uint32_t)g + t->last_d;
+        dst[0] = g + t->last_d;
     } else {
         dst[0] = (int32_t)(-t->L1 * d);
     }
@@ -1207,32 +1224,48 @@ int nw_table_copy_codes(nw_table* t, int64_t i0, int64_t i1, uint8_t* dst) {
     return NW_OK;
 }
 
-int nw_table_hash(nw_table* t, uint64_t* hH, uint64_t* hD) {
-    if (!t) return fail(NW_ERR_ARG, "nw_table_hash: NULL table");
-    if (!t->filled || !(t->last_mask & NW_OUT_SCORES)) return fail(NW_ERR_STATE, "nw_table_hash: no score table");
+int nw_table_hash_columns(nw_table* t, int64_t j0, uint64_t* hstate, uint64_t* dstate) {
+    if (!t || !hstate || !dstate || j0 < 0) return fail(NW_ERR_ARG, "nw_table_hash_columns: bad arguments");
+    if (!t->filled || !(t->last_mask & NW_OUT_SCORES))
+        return fail(NW_ERR_STATE, "nw_table_hash_columns: no score table");
     HIPCHK(hipSetDevice(t->device));
     const int64_t ncol = t->L1 + 1;
     uint64_t* dh = nullptr;
     HIPCHK(hipMalloc(&dh, (size_t)ncol * 16));
-    const bool have_d = (t->last_mask & NW_OUT_DIRS) != 0;
     TableView v = view_of(t);
-    if (!have_d) v.D = nullptr;
-    nw_colhash_kernel<<<(unsigned)((ncol + 255) / 256), 256, 0, t->stream>>>(v, (int32_t)t->L1, (int32_t)t->L2, dh,
-                                                                              dh + ncol);
-    std::vector<uint64_t> hv((size_t)ncol * 2);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpyAsync(hv.data(), dh, (size_t)ncol * 16, hipMemcpyDeviceToHost, t->stream);
+    if (!(t->last_mask & NW_OUT_DIRS)) v.D = nullptr;
+    hipError_t e = hipMemcpyAsync(dh, hstate, (size_t)ncol * 8, hipMemcpyHostToDevice, t->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dh + ncol, dstate, (size_t)ncol * 8, hipMemcpyHostToDevice, t->stream);
+    if (e == hipSuccess) {
+        nw_colhash_kernel<<<(unsigned)((ncol + 255) / 256), 256, 0, t->stream>>>(v, (int32_t)t->L1, (int32_t)t->L2,
+                                                                                  (int32_t)std::min<int64_t>(j0, t->L2 + 1),
+                                                                                  dh, dh + ncol);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(hstate, dh, (size_t)ncol * 8, hipMemcpyDeviceToHost, t->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dstate, dh + ncol, (size_t)ncol * 8, hipMemcpyDeviceToHost, t->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(t->stream);
     (void)hipFree(dh);
-    if (e != hipSuccess) return fail(NW_ERR_HIP, std::string("nw_table_hash: ") + hipGetErrorString(e));
-    auto fold = [](const uint64_t* v, int64_t n) {
-        uint64_t h = 0xcbf29ce484222325ULL;
-        for (int64_t i = 0; i < n; ++i)
-            for (int b = 0; b < 8; ++b) h = (h ^ ((v[i] >> (8 * b)) & 0xff)) * 0x100000001b3ULL;
-        return h;
-    };
-    if (hH) *hH = fold(hv.data(), ncol);
-    if (hD) *hD = have_d ? fold(hv.data() + ncol, ncol) : 0;
+    if (e != hipSuccess) return fail(NW_ERR_HIP, std::string("nw_table_hash_columns: ") + hipGetErrorString(e));
+    return NW_OK;
+}
+
+uint64_t nw_hash_fold(const uint64_t* state, int64_t n) {
+    uint64_t h = 0xcbf29ce484222325ULL;
+    for (int64_t i = 0; state && i < n; ++i)
+        for (int b = 0; b < 8; ++b) h = (h ^ ((state[i] >> (8 * b)) & 0xff)) * 0x100000001b3ULL;
+    return h;
+}
+
+int nw_table_hash(nw_table* t, uint64_t* hH, uint64_t* hD) {
+    if (!t) return fail(NW_ERR_ARG, "nw_table_hash: NULL table");
+    if (!t->filled || !(t->last_mask & NW_OUT_SCORES)) return fail(NW_ERR_STATE, "nw_table_hash: no score table");
+    const int64_t ncol = t->L1 + 1;
+    std::vector<uint64_t> hs((size_t)ncol, 0xcbf29ce484222325ULL), ds((size_t)ncol, 0xcbf29ce484222325ULL);
+    const int rc = nw_table_hash_columns(t, 0, hs.data(), ds.data());
+    if (rc) return fail(rc, std::string("nw_table_hash: ") + nw_last_error());
+    if (hH) *hH = nw_hash_fold(hs.data(), ncol);
+    if (hD) *hD = (t->last_mask & NW_OUT_DIRS) ? nw_hash_fold(ds.data(), ncol) : 0;
     return NW_OK;
 }
 

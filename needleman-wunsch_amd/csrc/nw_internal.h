@@ -43,6 +43,10 @@ struct nw_table {
     uint32_t* xflag = nullptr;      // host-visible block flags, or null
     int64_t xblk = 0;               // chunks per hand-off block
     uint32_t epoch = 0;             // tag of the fill in flight
+    int32_t* row0 = nullptr;        // device: the row above (H - d per column), snapshot by the loader
+    uint32_t* xin_credit = nullptr;       // consumer: where it posts "row above read" (FillArgs)
+    const uint32_t* xout_credit = nullptr;// producer: its consumer's xin_credit
+    uint32_t credit_want = 0;             // producer: the epoch xout_credit must read
     // fill in flight (between fill_launch and fill_finish)
     bool launched = false;
     uint32_t pend_mask = 0;

@@ -48,6 +48,16 @@ struct FillArgs {
     uint64_t* xout;         // bottom row granules for the panel below, or null
     uint32_t* xflag;        // host-visible: xflag[b] = epoch once block b of xout is written
     int32_t xblk;           // chunks per block
+    // Panel back-pressure (IPC / group transports; null otherwise).  The
+    // consumer snapshots the row above into row0 (H - d per column) while its
+    // loader reads xin, then posts this fill's epoch to xin_credit; the
+    // producer's first xout store of a fill waits until xout_credit (the
+    // consumer's xin_credit) reads credit_want, the epoch of its previous
+    // fill -- so a producer never overwrites a row its consumer still reads.
+    int32_t* row0;
+    uint32_t* xin_credit;
+    const uint32_t* xout_credit;
+    uint32_t credit_want;
 };
 
 // ---------------------------------------------------------------- DPP helpers
@@ -77,6 +87,35 @@ constexpr int SLOT = 16;
 __device__ __forceinline__ uint64_t ld_gran(const uint64_t* p, bool sys) {
     return sys ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Producer side of the panel back-pressure (FillArgs.xout_credit): one wave
+// waits until the consumer has read the previous fill's boundary row.  False
+// when the fill is being aborted (another wave's failure, or this wait's
+// watchdog: NW_ERR_TIMEOUT).
+__device__ __forceinline__ bool xcredit_wait(const FillArgs& a, const int* sh_abort) {
+    if (!a.xout_credit) return true;
+    const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const uint32_t c = __hip_atomic_load(a.xout_credit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (__builtin_amdgcn_readfirstlane((int)c) == (int)a.credit_want) return true;
+        const uint32_t ab = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ab || __hip_atomic_load(sh_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+        if ((int64_t)__builtin_amdgcn_s_memrealtime() - t0 > a.spin_ticks) {
+            if ((threadIdx.x & 63) == 0) {
+                __hip_atomic_store(&a.ctl[CTL_ABORT], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicCAS(&a.ctl[CTL_ERR], 0u, (uint32_t)NW_ERR_TIMEOUT);
+            }
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
+// Consumer side: the row above is read (and kept in row0); release xin.
+__device__ __forceinline__ void xcredit_post(const FillArgs& a) {
+    if (a.xin_credit && (threadIdx.x & 63) == 0)
+        __hip_atomic_store(a.xin_credit, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // LDS counters of the barrier-free intra-workgroup pipeline.

@@ -162,6 +162,10 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
             uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
             const int* bot = &tring[nw * R * SLOT];
             int cd = 0;
+            if (xpublish && !xcredit_wait(a, &sh_abort)) {
+                if (lane == 0) __hip_atomic_store(&sh_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                cd = NC;
+            }
             while ((publish || xpublish) && cd < NC) {
                 const int p = uni(lds_ld(&ctr[2 * nw + 2]));          // prog of the last wave's ring
                 if (p <= cd) {
@@ -258,6 +262,7 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                     if (lds_ld(&sh_abort)) break;
                     // H - d of the row above -> G' of row -1: + (i - base)*d
                     if (mine) dst[wb] = (int)(uint32_t)pf + (CH * c + wb + 1 - base) * d;
+                    if (xsrc && mine && wb < n) a.row0[CH * c + wb] = (int)(uint32_t)pf;
                 }
                 if (chl) {
                     dst[lane] = (int)pc;
@@ -266,6 +271,7 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                 lds_order();
                 if (lane == 0) lds_publish(&ctr[2], c + 1);
             }
+            if (xsrc) xcredit_post(a);
         } else if (real) {
             // ---------------- compute wave: its 128-row stripe, chunk by chunk ----
             // virtual 64-row stripes 2g (rows a) and 2g+1 (rows b): a.spitch = 1024*NC

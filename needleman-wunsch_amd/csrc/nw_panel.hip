@@ -88,8 +88,8 @@ namespace {
 int panel_alloc(nw_panel* p, int64_t max_L1, int64_t max_L2, uint32_t out_mask) {
     p->max_L1 = max_L1;
     p->max_L2 = max_L2;
-    const int64_t NGmax = cdiv(max_L2, 64);
-    const int64_t rows_cap = 64 * std::max<int64_t>(cdiv(NGmax, p->nranks), 1);
+    const int64_t NGmax = cdiv(max_L2, 128);
+    const int64_t rows_cap = 128 * std::max<int64_t>(cdiv(NGmax, p->nranks), 1);
     int rc = nw_table_create(p->device, max_L1, std::min(rows_cap, std::max<int64_t>(max_L2, 0)), out_mask, &p->t);
     if (rc) return rc;
     NW_HIPCHK(hipSetDevice(p->device));
@@ -98,8 +98,10 @@ int panel_alloc(nw_panel* p, int64_t max_L1, int64_t max_L2, uint32_t out_mask) 
     // The boundary buffer is written by another agent (a peer GPU over xGMI,
     // another process, RCCL): uncached device memory, so the loader's polls
     // can never hit a stale L2 line.
-    NW_HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&p->xin), (size_t)p->xcap * 8, hipDeviceMallocUncached));
-    NW_HIPCHK(hipMemset(p->xin, 0, (size_t)p->xcap * 8));
+    // One more 64-byte line after the granules: this panel's credit word
+    // (credit_of), the back-pressure of the IPC / group transports.
+    NW_HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&p->xin), (size_t)p->xcap * 8 + 64, hipDeviceMallocUncached));
+    NW_HIPCHK(hipMemset(p->xin, 0, (size_t)p->xcap * 8 + 64));
     NW_HIPCHK(hipStreamCreateWithFlags(&p->s_send, hipStreamNonBlocking));
     if (p->transport == NW_PANEL_RCCL) {
         p->xblk = xblk_chunks();
@@ -128,11 +130,20 @@ void make_record(const nw_panel* p, int64_t* rec) {
     rec[6] = p->rows;
 }
 
-void configure(nw_panel* p, uint32_t epoch) {
+// The credit word behind a boundary buffer of xcap granules: the epoch of
+// the last fill whose row above its owner has finished reading.
+uint32_t* credit_of(uint64_t* xin, int64_t xcap) { return reinterpret_cast<uint32_t*>(xin + xcap); }
+
+// prev_epoch: the epoch of this panel's previous fill (0 before the first).
+void configure(nw_panel* p, uint32_t epoch, uint32_t prev_epoch) {
     nw_table* t = p->t;
+    const bool credits = p->transport != NW_PANEL_RCCL;   // RCCL's own send/recv pairing paces it
     t->epoch = epoch;
     t->xin = (p->prev >= 0 && p->rows > 0) ? p->xin : nullptr;
+    t->xin_credit = credits ? credit_of(p->xin, p->xcap) : nullptr;
     t->xout = nullptr;
+    t->xout_credit = nullptr;
+    t->credit_want = prev_epoch;
     t->xflag = nullptr;
     t->xblk = p->xblk;
     if (p->next >= 0 && p->rows > 0) {
@@ -142,7 +153,19 @@ void configure(nw_panel* p, uint32_t epoch) {
             t->xout = p->xout;
             t->xflag = p->xflag_dev;
         }
+        if (credits) t->xout_credit = credit_of(t->xout, p->xcap);
     }
+}
+
+// Every panel posts its credit for every fill: a fill kernel that reads the
+// row above posts it itself once read (xcredit_post); otherwise it is posted
+// here, stream-ordered after this panel's work, so a producer never waits on
+// a panel that has nothing to read (first panel, empty panel, L1 == 0).
+int post_credit(nw_panel* p, bool kernel_posts) {
+    if (p->transport == NW_PANEL_RCCL || kernel_posts) return NW_OK;
+    NW_HIPCHK(hipSetDevice(p->device));
+    NW_HIPCHK(hipMemsetD32Async(credit_of(p->xin, p->xcap), (int)p->epoch, 1, p->t->stream));
+    return NW_OK;
 }
 
 uint32_t next_epoch(uint32_t e) { return e >= kEpochMax ? 1u : e + 1u; }
@@ -167,10 +190,11 @@ extern "C" {
 int nw_panel_partition(int64_t L2, int nranks, int rank, int64_t* row_base, int64_t* rows) {
     if (L2 < 0 || nranks < 1 || rank < 0 || rank >= nranks || !row_base || !rows)
         return fail(NW_ERR_ARG, "nw_panel_partition: bad arguments");
-    const int64_t NG = cdiv(L2, 64);
+    // whole 128-row pair stripes, so every feeding panel can run the pair kernel
+    const int64_t NG = cdiv(L2, 128);
     const int64_t g0 = NG * rank / nranks, g1 = NG * (rank + 1) / nranks;
-    *row_base = std::min(64 * g0, L2);
-    *rows = std::max<int64_t>(0, std::min(64 * g1, L2) - *row_base);
+    *row_base = std::min(128 * g0, L2);
+    *rows = std::max<int64_t>(0, std::min(128 * g1, L2) - *row_base);
     return NW_OK;
 }
 
@@ -363,12 +387,13 @@ int nw_panel_fill(nw_panel* p, int32_t m, int32_t k, int32_t d, uint32_t out_mas
         return fail(NW_ERR_STATE, "nw_panel_fill: RCCL panel has no communicator");
     const double t0 = now_ms();
     NW_HIPCHK(hipSetDevice(p->device));
+    const uint32_t prev_epoch = p->epoch;
     p->epoch = next_epoch(p->epoch);
     const uint32_t epoch = p->epoch;
     p->filled = false;
     p->have_global = false;
     p->last_d = d;
-    configure(p, epoch);
+    configure(p, epoch, prev_epoch);
     nw_table* t = p->t;
     int rc = NW_OK;
     bool launched = false;
@@ -376,6 +401,7 @@ int nw_panel_fill(nw_panel* p, int32_t m, int32_t k, int32_t d, uint32_t out_mas
         rc = nwi::fill_launch(t, m, k, d, out_mask);
         launched = rc == NW_OK;
     }
+    if (rc == NW_OK) rc = post_credit(p, launched && t->xin);
     const int64_t NC = cdiv(p->L1, kChunk);
     const int64_t NB = (p->rows > 0 && p->L1 > 0) ? cdiv(NC, p->xblk) : 0;
     auto blk = [&](int64_t b, int64_t* off, int64_t* cnt) {
@@ -451,14 +477,15 @@ int nw_panel_group_fill(nw_panel* const* ps, int n, int32_t m, int32_t k, int32_
         if (!p->have_seq) return fail(NW_ERR_STATE, "nw_panel_group_fill: no sequences set");
     }
     const double t0 = now_ms();
-    const uint32_t epoch = next_epoch(ps[0]->epoch);
+    const uint32_t prev_epoch = ps[0]->epoch;
+    const uint32_t epoch = next_epoch(prev_epoch);
     for (int r = 0; r < n; ++r) {
         nw_panel* p = ps[r];
         p->epoch = epoch;
         p->filled = false;
         p->have_global = false;
         p->last_d = d;
-        configure(p, epoch);
+        configure(p, epoch, prev_epoch);
     }
     // Launch top-down (a panel only ever waits on panels launched before it),
     // then complete top-down, poisoning the row a failed panel owes.
@@ -476,6 +503,7 @@ int nw_panel_group_fill(nw_panel* const* ps, int n, int32_t m, int32_t k, int32_
             launched[(size_t)r] = rcs[(size_t)r] == NW_OK;
             if (!launched[(size_t)r]) stop = true;
         }
+        if (rcs[(size_t)r] == NW_OK) rcs[(size_t)r] = post_credit(p, launched[(size_t)r] && p->t->xin);
     }
     for (int r = 0; r < n; ++r) {
         nw_panel* p = ps[r];
@@ -545,6 +573,14 @@ int nw_panel_stats(nw_panel* p, nw_stats* st) {
                                       : "nw_panel_stats: gather nw_panel_record()s and use nw_panel_reduce()");
     *st = p->stats;
     return NW_OK;
+}
+
+int nw_panel_hash_columns(nw_panel* p, uint64_t* hstate, uint64_t* dstate) {
+    if (!p || !hstate || !dstate) return fail(NW_ERR_ARG, "nw_panel_hash_columns: bad arguments");
+    if (!p->filled || p->last_rc != NW_OK) return fail(NW_ERR_STATE, "nw_panel_hash_columns: no completed fill");
+    if (p->rows == 0) return NW_OK;   // no rows of its own
+    // the first panel hashes global row 0 (the seed) too; the others start at their first own row
+    return nw_table_hash_columns(p->t, p->row_base == 0 ? 0 : 1, hstate, dstate);
 }
 
 int nw_panel_rows(const nw_panel* p, int64_t* row_base, int64_t* rows) {

@@ -229,6 +229,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
                     }
                     if (lds_ld(&sh_abort)) break;
                     if (mine) dst[wb] = (int)(uint32_t)pf + d;                 // granules carry H - d
+                    if (xsrc && mine && wb < n && CH * c + wb < a.L1) a.row0[CH * c + wb] = (int)(uint32_t)pf;
                 }
                 // window: copy k holds column p + 1 + k at position p
                 swin[wk * SWN + ((CH * c + wb - wk) & (SWN - 1))] = pc;
@@ -236,6 +237,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
                 lds_order();
                 if (lane == 0) lds_publish(&ctr[2], c + 9);   // prog = slots done + 8
             }
+            if (xsrc) xcredit_post(a);
         } else if (real) {
             // ---------------- compute wave: its 64-row stripe, 8 steps per chunk ----
             uint64_t* gout = a.gran + (int64_t)((sidx + 1) % a.nslot) * a.gpitch;
@@ -244,6 +246,8 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
             int hv = lane * 16, dv = lane * 4;                         // byte offsets from hb / db
             const bool publish = (w == nw - 1) && sidx + 1 < a.NSW;
             const bool xpublish = a.xout && g == a.NG - 1;
+            if (xpublish && !xcredit_wait(a, &sh_abort) && lane == 0)
+                __hip_atomic_store(&sh_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             const bool out_lane = jrow <= a.L2;
             const int* tin = &tring[w * R * SLOT];
             int* tout = &tring[(w + 1) * R * SLOT];

@@ -57,12 +57,12 @@ EXPORTS = (
     "nw_table_stats", "nw_table_elapsed_ms", "nw_table_hash", "nw_table_copy_scores",
     "nw_table_copy_codes", "nw_table_copy_last_column", "nw_table_score_pitch", "nw_table_waves",
     "nw_table_trace", "nw_table_count_alignments", "nw_table_first_path", "nw_table_walk_elapsed_ms",
-    "nw_first_path_banded",
+    "nw_first_path_banded", "nw_table_hash_columns", "nw_hash_fold",
     # include/nw_panel.h
     "nw_panel_partition", "nw_panel_chain", "nw_panel_get_id", "nw_panel_create", "nw_panel_ipc_handle",
     "nw_panel_ipc_connect", "nw_panel_group_create", "nw_panel_destroy", "nw_panel_set_sequences",
     "nw_panel_fill", "nw_panel_group_fill", "nw_panel_stats", "nw_panel_record", "nw_panel_reduce",
-    "nw_panel_rows", "nw_panel_table", "nw_panel_elapsed_ms",
+    "nw_panel_rows", "nw_panel_table", "nw_panel_elapsed_ms", "nw_panel_hash_columns",
 )
 
 
@@ -148,6 +148,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "nw_panel_rows": (c_int, [c_p, P(c_i64), P(c_i64)]),
         "nw_panel_table": (c_p, [c_p]),
         "nw_panel_elapsed_ms": (c_int, [c_p, P(ctypes.c_float), P(ctypes.c_float)]),
+        "nw_panel_hash_columns": (c_int, [c_p, c_p, c_p]),
+        "nw_table_hash_columns": (c_int, [c_p, c_i64, c_p, c_p]),
+        "nw_hash_fold": (ctypes.c_uint64, [c_p, c_i64]),
         "nw_table_count_alignments": (c_int, [c_p, P(c_u32)]),
         "nw_table_first_path": (c_int, [c_p, c_p, c_i64, P(c_i64)]),
         "nw_table_walk_elapsed_ms": (c_int, [c_p, P(ctypes.c_float), P(ctypes.c_float)]),
@@ -266,6 +269,11 @@ class Table:
         a, b = ctypes.c_uint64(), ctypes.c_uint64()
         _check(self._lib.nw_table_hash(self._h, ctypes.byref(a), ctypes.byref(b)), "nw_table_hash")
         return a.value, b.value
+
+    def hash_columns(self, j0: int, state: np.ndarray) -> None:
+        """Continue per-column FNV states (2, L1+1) uint64 -- scores, codes -- over rows j0..L2."""
+        _check(self._lib.nw_table_hash_columns(self._h, j0, state[0].ctypes.data, state[1].ctypes.data),
+               "nw_table_hash_columns")
 
     def scores(self, i0: int = 0, i1: int | None = None) -> np.ndarray:
         i1 = self.L1 + 1 if i1 is None else i1
@@ -456,6 +464,23 @@ class Panel:
         a, b = ctypes.c_float(), ctypes.c_float()
         _check(self._lib.nw_panel_elapsed_ms(self._h, ctypes.byref(a), ctypes.byref(b)), "nw_panel_elapsed_ms")
         return a.value, b.value
+
+    def hash_columns(self, state: np.ndarray) -> None:
+        """Continue the whole table's per-column FNV states (see hash_states) over this panel's rows."""
+        _check(self._lib.nw_panel_hash_columns(self._h, state[0].ctypes.data, state[1].ctypes.data),
+               "nw_panel_hash_columns")
+
+
+def hash_states(L1: int) -> np.ndarray:
+    """Fresh per-column FNV-1a-64 states for a table of L1+1 columns: row 0 = scores, row 1 = codes."""
+    return np.full((2, L1 + 1), 0xCBF29CE484222325, dtype=np.uint64)
+
+
+def hash_fold(state: np.ndarray) -> tuple[int, int]:
+    """(hH, hD) of nw_table_hash from chained per-column states (Panel.hash_columns)."""
+    lib = load()
+    st = np.ascontiguousarray(state, dtype=np.uint64)
+    return int(lib.nw_hash_fold(st[0].ctypes.data, st.shape[1])), int(lib.nw_hash_fold(st[1].ctypes.data, st.shape[1]))
 
 
 def render_path(s1, s2, moves) -> tuple[bytes, bytes]:

@@ -9,6 +9,7 @@ panel on `device` (several ranks on one GPU rehearse the hipIpc path).  Rank
 """
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -27,9 +28,18 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     p = bench_multi.make_panel(transport, rank, world, device, L1, L2, nw_amd.NW_OUT_ALL)
     p.set_sequences(nw_amd.gen_dna(1, L1), nw_amd.gen_dna(2, L2))
+    # NW_TEST_MKD_SEQ="m,k,d;m,k,d;..." runs those fills back to back (the
+    # last one is checked); NW_TEST_DELAY="rank:seconds" makes that rank start
+    # every fill late, so the panel above runs ahead and must wait for its
+    # credit instead of overwriting a boundary row still being read.
+    seq = [tuple(map(int, x.split(","))) for x in os.environ.get("NW_TEST_MKD_SEQ", "").split(";") if x]
+    seq = seq or [(m, k, d)] * int(os.environ.get("NW_TEST_FILLS", "2"))
+    delay_rank, delay_s = (os.environ.get("NW_TEST_DELAY", "-1:0").split(":") + ["0"])[:2]
     rcs = []
-    for _ in range(int(os.environ.get("NW_TEST_FILLS", "2"))):
-        rcs.append(p.fill_rc(m, k, d, nw_amd.NW_OUT_ALL))
+    for mkd in seq:
+        if int(delay_rank) == rank:
+            time.sleep(float(delay_s))
+        rcs.append(p.fill_rc(*mkd, nw_amd.NW_OUT_ALL))
     base, rows = p.rows()
     t = p.table
     payload = {"rank": rank, "base": base, "rows": rows, "rcs": rcs}
@@ -44,7 +54,8 @@ def main():
         np.savez(out, rc=rc, stats=np.array([st.corner, st.greatest_abs_interior, st.branch_count], dtype=np.int64),
                  **{f"H{r['rank']}": r["H"] for r in allp if "H" in r},
                  **{f"D{r['rank']}": r["D"] for r in allp if "D" in r},
-                 meta=np.array([[r["rank"], r["base"], r["rows"], r["rcs"][-1]] for r in allp], dtype=np.int64))
+                 meta=np.array([[r["rank"], r["base"], r["rows"], next((x for x in r["rcs"] if x), 0)]
+                                   for r in allp], dtype=np.int64))
     dist.barrier()
     p.close()
     dist.destroy_process_group()

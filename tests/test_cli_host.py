@@ -24,9 +24,10 @@ def _built():
         subprocess.check_call(["make", "-s", "-C", PKG, "cli", "hostlib"])
 
 
-def run_cli(case):
+def run_cli(case, binary=None):
     """Run the CLI as `needleman-wunsch` (argv[0] matters, dbg.c:7-15)."""
-    _built()
+    if binary is None:
+        _built()
     args, stdin, tmp = list(case["args"]), case["stdin"], None
     if "{FILE}" in args:
         tmp = tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False)
@@ -35,7 +36,7 @@ def run_cli(case):
         args = [tmp.name if a == "{FILE}" else a for a in args]
         stdin = ""
     try:
-        p = subprocess.run(["needleman-wunsch"] + args, executable=CLI, input=stdin.encode(),
+        p = subprocess.run(["needleman-wunsch"] + args, executable=binary or CLI, input=stdin.encode(),
                            capture_output=True, timeout=300)
     finally:
         if tmp:

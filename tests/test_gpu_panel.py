@@ -136,18 +136,42 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("L1,L2,mkd", [(2000, 1500, (2, 3, 5)), (500, 100, (1, 1, 1))])
-def test_ipc_two_processes(tmp_path, L1, L2, mkd):
-    """Two processes, one panel each, on device 0, boundary over hipIpc."""
+def _run_ipc(tmp_path, L1, L2, mkd, world=2, extra_env=None):
     out = str(tmp_path / "ipc.npz")
     port = _free_port()
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   **(extra_env or {}))
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "panel_ipc_worker.py"), out,
                                        str(L1), str(L2), *map(str, mkd), "ipc", "0"], env=env))
-    rcs = [p.wait(timeout=300) for p in procs]
-    assert rcs == [0, 0]
+    rcs = [p.wait(timeout=100) for p in procs]
+    assert rcs == [0] * world
+    return out
+
+
+@pytest.mark.parametrize("L1,L2,mkd", [(2000, 1500, (2, 3, 5)), (500, 100, (1, 1, 1))])
+def test_ipc_two_processes(tmp_path, L1, L2, mkd):
+    """Two processes, one panel each, on device 0, boundary over hipIpc."""
+    out = _run_ipc(tmp_path, L1, L2, mkd)
+    _check_ipc(out, L1, L2, mkd)
+
+
+@pytest.mark.parametrize("delay_rank,world", [(1, 2), (2, 3)])
+def test_ipc_back_to_back_delayed_consumer(tmp_path, delay_rank, world):
+    """Back-to-back fills with different m, k, d while one consumer starts
+    every fill 0.4 s late: the panels above run ahead into the next fill and
+    must wait for its credit (without back-pressure the producer
+    overwrote a boundary row still being read, and the consumer timed out)."""
+    L1, L2 = 3000, 1000
+    seq = [(2, 3, 5), (1, 1, 1), (3, 1, 2), (1, 2, 1)]
+    out = _run_ipc(tmp_path, L1, L2, seq[-1], world,
+                   {"NW_TEST_MKD_SEQ": ";".join(",".join(map(str, x)) for x in seq),
+                    "NW_TEST_DELAY": f"{delay_rank}:0.4"})
+    _check_ipc(out, L1, L2, seq[-1])
+
+
+def _check_ipc(out, L1, L2, mkd):
     z = np.load(out)
     s1, s2 = O.gen_dna(1, L1), O.gen_dna(2, L2)
     H, D, st = O.fill(s1, s2, *mkd)

@@ -29,15 +29,15 @@ def test_partition_covers_rows(L2, n):
     sizes = []
     for r, (base, rows) in enumerate(parts):
         assert base == pos or rows == 0
-        assert base % 64 == 0 or rows == 0
+        assert base % 128 == 0 or rows == 0
         pos = base + rows if rows else pos
         sizes.append(rows)
     assert pos == L2 and sum(sizes) == L2
     nonempty = [i for i, s in enumerate(sizes) if s]
     for i in nonempty[:-1]:
-        assert sizes[i] % 64 == 0, "a feeding panel must hold whole 64-row stripes"
+        assert sizes[i] % 128 == 0, "a feeding panel must hold whole 128-row stripes"
     if nonempty:
-        stripes = [-(-sizes[i] // 64) for i in range(n)]
+        stripes = [-(-sizes[i] // 128) for i in range(n)]
         assert max(stripes) - min(stripes) <= 1
 
 

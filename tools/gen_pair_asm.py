@@ -292,6 +292,8 @@ def main():
     for HH, FF, ST in ((1, 1, 1), (1, 1, 0), (1, 0, 0), (0, 1, 0), (0, 0, 0)):
         for P in (0, 1):
             lines = block(ST, P, HH, FF)
+            nvalu = sum(1 for x in lines if x.startswith("v_"))
+            parts.append(f"// VALU pair_chunk_asm<{tf(HH)}, {tf(FF)}, {tf(ST)}, {tf(P)}>: {nvalu} per 8 columns x 128 rows\n")
             parts.append(
                 f"template <> __device__ __forceinline__ void pair_chunk_asm<{tf(HH)}, {tf(FF)}, {tf(ST)}, {tf(P)}>"
                 f"(PairRegs& r, const PairConst& k, const PairSlot& ts, PairSlot& ns, int cv, int ra, int rd) {{\n"

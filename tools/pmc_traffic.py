@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 output of tools/profile_round.sh into profiles/.
 
-    python tools/pmc_traffic.py ROUND OUTDIR L1 L2
+    python tools/pmc_traffic.py ROUND OUTDIR L1 L2 [WARMUP]
 
 OUTDIR holds three rocprofv3 runs of `bench.py` (same workload):
-  kt/   --kernel-trace --stats        -> per-kernel average duration
+  kt/   --kernel-trace --stats        -> per-kernel average duration; the
+        steady-state average skips the first WARMUP fill launches (bench.py's
+        untimed warm-up), which is what bench.py's HIP-event kernel_ms covers;
+        kt.log holds the bench line printed under the profiler
   wr/   --pmc WRITE_SIZE              -> HBM write bytes per fill launch
   rd/   --pmc FETCH_SIZE              -> HBM read bytes per fill launch
 Counters come from separate passes (TCC slots: FETCH_SIZE costs 3,
@@ -65,6 +68,22 @@ def main():
             if is_fill(r["Name"]):
                 avg_ns = float(r["AverageNs"])
                 name = r["Name"]
+    warm = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+    durs = []
+    with open(find(os.path.join(out, "kt"), "*kernel_trace.csv")) as f:
+        rows = [r for r in csv.DictReader(f) if is_fill(r["Kernel_Name"])]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in rows]
+    steady = durs[warm:] if len(durs) > warm else durs
+    steady_ns = sum(steady) / len(steady)
+    bench_line = None
+    try:
+        with open(os.path.join(out, "kt.log")) as f:
+            for ln in f:
+                if ln.startswith("{") and '"metric"' in ln:
+                    bench_line = json.loads(ln)
+    except OSError:
+        pass
     wr_kib, nw, wsrc = counter_per_launch(os.path.join(out, "wr"), "WRITE_SIZE")
     rd_kib, nr, rsrc = counter_per_launch(os.path.join(out, "rd"), "FETCH_SIZE")
     write_b = wr_kib * 1024
@@ -72,6 +91,13 @@ def main():
     alg = 4.5 * (L1 + 1) * (L2 + 1)
     j = {
         "round": rnd, "L1": L1, "L2": L2, "kernel": name, "avg_kernel_ns": avg_ns,
+        "launches_traced": len(durs), "warmup_launches_skipped": min(warm, len(durs)),
+        "steady_avg_kernel_ns": steady_ns, "steady_min_kernel_ns": min(steady), "steady_max_kernel_ns": max(steady),
+        "alg_gbs_steady": 4.5 * (L1 + 1) * (L2 + 1) / steady_ns,
+        "bench_line_under_profiler": None if bench_line is None else {
+            "ms_per_step": bench_line.get("ms_per_step"),
+            "kernel_ms": bench_line.get("roofline", {}).get("kernel_ms"),
+            "frac": bench_line.get("roofline", {}).get("frac")},
         "write_bytes_per_launch": write_b, "fetch_bytes_per_launch": fetch_b,
         "hbm_bytes_per_launch": write_b + fetch_b,
         "alg_bytes_per_launch": alg, "traffic_over_alg": (write_b + fetch_b) / alg,
