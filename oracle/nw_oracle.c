@@ -404,7 +404,10 @@ uint32_t nwo_count_paths(const uint8_t *D, int64_t L1, int64_t L2)
                 prev = cur;
                 cur = t;
         }
-        const uint32_t r = prev[L2];
+        /* Two empty strings: the walk starts on (0,0), whose three directions
+           init_computation marked done (computation.c:96-99), so its loop
+           (needleman-wunsch.c:231-235) never runs and nothing is counted. */
+        const uint32_t r = (L1 == 0 && L2 == 0) ? 0u : prev[L2];
         free(prev);
         free(cur);
         return r;

@@ -16,7 +16,7 @@ OUT=gpurun_out/prof_$RND
 export TMPDIR=/tmp
 rm -rf "$OUT"
 mkdir -p "$OUT"
-B=(bench.py --L1 "$L1" --L2 "$L2" --no-cpu-baseline)
+B=(bench.py --L1 "$L1" --L2 "$L2" --no-cpu-baseline --no-c2)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
     python3 "${B[@]}" --steps 20 --warmup 5 > "$OUT/kt.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/wr" -o run -- \
