@@ -86,6 +86,10 @@ def main():
         pass
     wr_kib, nw, wsrc = counter_per_launch(os.path.join(out, "wr"), "WRITE_SIZE")
     rd_kib, nr, rsrc = counter_per_launch(os.path.join(out, "rd"), "FETCH_SIZE")
+    # the raw per-dispatch counter rows and the kernel trace travel with the summary
+    shutil.copy(find(os.path.join(out, "wr"), "*counter_collection.csv"), os.path.join(out, f"{rnd}_pmc_write_size.csv"))
+    shutil.copy(find(os.path.join(out, "rd"), "*counter_collection.csv"), os.path.join(out, f"{rnd}_pmc_fetch_size.csv"))
+    shutil.copy(find(os.path.join(out, "kt"), "*kernel_trace.csv"), os.path.join(out, f"{rnd}_kernel_trace.csv"))
     write_b = wr_kib * 1024
     fetch_b = 2 * rd_kib * 1024
     alg = 4.5 * (L1 + 1) * (L2 + 1)
@@ -104,7 +108,7 @@ def main():
         "hbm_gbs_from_counters": (write_b + fetch_b) / avg_ns if avg_ns else None,
         "launches": {"WRITE_SIZE": nw, "FETCH_SIZE": nr},
         "correction": "WRITE_SIZE*1024 + 2*FETCH_SIZE*1024 (gfx950 FETCH_SIZE halves wide streams)",
-        "sources": {"stats": f"profiles/{rnd}_kernel_stats.csv", "write": f"profiles/{rnd}_pmc_write_size.csv", "fetch": f"profiles/{rnd}_pmc_fetch_size.csv"},
+        "sources": {"stats": f"profiles/{rnd}_kernel_stats.csv", "trace": f"profiles/{rnd}_kernel_trace.csv", "write": f"profiles/{rnd}_pmc_write_size.csv", "fetch": f"profiles/{rnd}_pmc_fetch_size.csv"},
     }
     with open(os.path.join(out, f"{rnd}_pmc_traffic.json"), "w") as f:
         json.dump(j, f, indent=1)
