@@ -37,6 +37,7 @@
 #ifndef NW_FILL_H
 #define NW_FILL_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -145,6 +146,22 @@ int nw_table_copy_scores(nw_table *t, int64_t i0, int64_t i1, int32_t *dst);
 int nw_table_copy_codes(nw_table *t, int64_t i0, int64_t i1, uint8_t *dst);
 /* Copy the last column H[L1][0..L2] (available in score-only mode too). */
 int nw_table_copy_last_column(nw_table *t, int32_t *dst);
+/* Slice copies are streamed: gather kernels fill two device staging buffers
+ * while the DMA of the previous block runs.  A destination in pinned memory
+ * (nw_host_alloc, or any hipHostMalloc'd / registered range) is written by
+ * the DMA directly, at PCIe rate; a pageable one goes through two pinned
+ * bounce buffers whose host copy overlaps the next DMA.  The reference holds
+ * the whole table in host memory (score-table.c:60-81); here only the slice
+ * a consumer asks for crosses PCIe.  nw_table_set_sequences likewise codes
+ * the sequences into pinned staging and uploads from there (the reference
+ * grows its input buffers in 4 KB steps, read-sequences.c:66-75). */
+int nw_host_alloc(size_t bytes, void **p);
+void nw_host_free(void *p);
+/* Wall-clock ms and bytes of the last upload (nw_table_set_sequences, symbol
+ * coding included) and of the last slice copy (nw_table_copy_scores /
+ * nw_table_copy_codes / nw_table_copy_last_column).  Any pointer may be NULL. */
+int nw_table_io_stats(nw_table *t, double *upload_ms, int64_t *upload_bytes, double *copy_ms,
+                      int64_t *copy_bytes);
 /* Geometry of the device layout (for zero-copy consumers). */
 int64_t nw_table_score_pitch(const nw_table *t);
 /* In-kernel timeline of the last fill, recorded only when $NW_TRACE is set:

@@ -78,6 +78,37 @@ int nw_panel_partition(int64_t L2, int nranks, int rank, int64_t *row_base, int6
  * that chain (-1 for an empty panel).  Pure host logic. */
 int nw_panel_chain(int64_t L2, int nranks, int rank, int *prev, int *next, int *pos);
 
+/* The RCCL transport's host proxy as pure host logic (no device needed), so
+ * its sequencing is testable anywhere.  One fill's boundary row of L1
+ * granules moves in blocks of xblk chunks (8 columns each; block b covers
+ * granules [b*8*xblk, min(L1, (b+1)*8*xblk))).  The proxy
+ *   1. posts every receive of the row above first (has_prev), so the panel
+ *      above never blocks on this one;
+ *   2. then (has_next), block by block in order, polls the producer kernel's
+ *      flag for the block and sends it; once the kernel has ended without the
+ *      block (flag() < 0, or launched == 0) it poisons that block and every
+ *      later one (tag = epoch | 2^31, see above) and still sends them, so the
+ *      panel below fails with NW_ERR_PEER instead of timing out.
+ * It stops at the first failing recv / send callback and returns its code
+ * (a poison failure is returned after that block is sent).  The callbacks:
+ *   recv(ctx, off, cnt), send(ctx, off, cnt), poison(ctx, off, cnt):
+ *        0 on success, an nw_err code otherwise;
+ *   flag(ctx, b, spin): 1 = block b is ready, 0 = not yet (called again with
+ *        spin + 1), -1 = the producer kernel ended without it.
+ * The RCCL transport's callbacks are ncclRecv / ncclSend on the panel's two
+ * communicators, the pinned per-block flag words and a poison kernel.  This
+ * is the role of the reference's per-cell wait on the left neighbour
+ * (needleman-wunsch.c:444-475), moved to one boundary row per panel. */
+typedef struct {
+        void *ctx;
+        int (*recv)(void *ctx, int64_t off, int64_t cnt);
+        int (*flag)(void *ctx, int64_t b, uint64_t spin);
+        int (*poison)(void *ctx, int64_t off, int64_t cnt);
+        int (*send)(void *ctx, int64_t off, int64_t cnt);
+} nw_panel_proxy_ops;
+int nw_panel_proxy_run(int64_t L1, int64_t xblk, int has_prev, int has_next, int launched,
+                       const nw_panel_proxy_ops *ops);
+
 /* RCCL only, rank 0: create the rendezvous id; the caller broadcasts it. */
 int nw_panel_get_id(uint8_t id[NW_PANEL_ID_BYTES]);
 

@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <type_traits>
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -275,11 +276,10 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
                     if (lane < n) {
                         // (plain domain: H - d = G' - 64*nw*d - (i - base)d)
                         const int v = bot[(cd % R) * SLOT + lane] - 64 * nw * d - (CH * cd + lane + 1 - chunk_base(cd)) * d;
-                        const uint64_t tag = publish ? (uint32_t)(sidx + 1) : a.epoch;
+                        const uint64_t tag = publish ? a.gtag | (uint32_t)(sidx + 1) : a.epoch;
                         const uint64_t gr = (tag << 32) | (uint32_t)v;
                         if (publish)
-                            __hip_atomic_store(gout + CH * (int64_t)cd + lane, gr, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
+                            put_granule(gout, CH * (int64_t)cd + lane, gr);
                         else
                             __hip_atomic_store(a.xout + CH * (int64_t)cd + lane, gr, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_SYSTEM);
@@ -299,18 +299,20 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
             // Source of the WG-stripe's top row: the seeded row 0, the panel
             // above (xin, written by another agent: system-scope loads), or
             // the previous WG-stripe's granules (agent scope).  Lanes 8, 9
-            // carry the chunk's top-string bytes.
+            // write the chunk's top-string bytes.
+            // Nothing it waits for per chunk is a fresh global load unless the
+            // granules are not there yet: the granule window (8 chunks, one lane
+            // per granule) and the top-string window (lanes 0..15: the 16 dwords
+            // of those 8 chunks) are prefetched one window ahead; a per-chunk
+            // dependent load made the loader, not the producer, pace every
+            // WG-stripe hop (+11% at 100k^2, tools/trace_lag.py).  Kept inline:
+            // the same loop as a shared __device__ function compiled 5-10%
+            // slower at 100k^2 (profiles/r02_ab_loader.txt; nw_pair.hip has the same loop).
             const bool seeded = sidx == 0 && !a.xin;
             const bool xsrc = sidx == 0 && a.xin;
             const uint64_t* gin = xsrc ? a.xin : a.gran + (int64_t)(sidx % a.nslot) * a.gpitch;
-            const uint32_t want = xsrc ? a.epoch : (uint32_t)sidx;
+            const uint32_t want = xsrc ? a.epoch : a.gtag | (uint32_t)sidx;
             const uint32_t* s1w = reinterpret_cast<const uint32_t*>(a.s1);
-            const bool chl = lane == 8 || lane == 9;
-            // Granule window: lane l holds granule (cw + l/8, column l%8), so
-            // one load covers 8 chunks and pn prefetches the next 8; a poll
-            // reloads only the lanes of chunks >= c that are not valid yet.
-            // (One chunk per load round trip made the loader, not the
-            // producer, pace a WG-stripe behind its predecessor.)
             const int wk = lane >> 3, wb = lane & 7;
             const int64_t ngr = (int64_t)CH * NC;
             auto gload = [&](int cf) -> uint64_t {
@@ -319,7 +321,12 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
             };
             int cw = 0;
             uint64_t pf = 0, pn = 0;
-            uint32_t pc = chl ? s1w[lane - 8] : 0u;
+            const int64_t nsw = 2 * (int64_t)NC + 16;
+            auto sload = [&](int cf) -> uint32_t {
+                const int64_t x = 2 * (int64_t)cf + lane;
+                return lane < 16 && x < nsw ? s1w[x] : 0u;
+            };
+            uint32_t sw = sload(0), swn = sload(CH);
             if (!seeded) {
                 pf = gload(0);
                 pn = gload(CH);
@@ -329,16 +336,21 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
                 if (c == cw + CH) {
                     cw += CH;
                     pf = pn;
+                    sw = swn;
                     if (!seeded) pn = gload(cw + CH);
+                    swn = sload(cw + CH);
                 }
-                while (lds_ld(&ctr[1]) < c - R + 1) __builtin_amdgcn_s_sleep(1);   // ring slot free?
+                const bool tcm = NW_TRACE_EXT && a.trace && lane == 0 && c == trace_mid_chunk(NC, R);
+                if (tcm) *trace_ext(a, TX_REACH, sidx) = __builtin_amdgcn_s_memrealtime();
+                while (lds_ld(&ctr[1]) < c - R + 1) __builtin_amdgcn_s_sleep(1);
+                if (tcm) *trace_ext(a, TX_CREDIT, sidx) = __builtin_amdgcn_s_memrealtime();
                 int* dst = &tring[(c % R) * SLOT];
                 const int base = chunk_base(c);
                 if (seeded) {
                     // row 0: H[i][0] - d = -(i+1)*d (computation.c:102-110) -> G' = -(base+1)*d
                     if (lane < CH) dst[lane] = -(base + 1) * d;
                 } else {
-                    const bool mine = wk == c - cw;           // this lane carries chunk c
+                    const bool mine = wk == c - cw;
                     bool ok = !mine || wb >= n || (uint32_t)(pf >> 32) == want;
                     if (!__all(ok)) {
                         const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
@@ -350,7 +362,6 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
                             const int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
                             const uint32_t ab = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED,
                                                                   __HIP_MEMORY_SCOPE_AGENT);
-                            // a failed panel above poisons its boundary row
                             const bool peer = xsrc && __any(mine && wb < n && (uint32_t)(pf >> 32) == (want | POISON_BIT));
                             if (ab || peer || now - t0 > a.spin_ticks) {
                                 if (lane == 0) {
@@ -366,14 +377,18 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
                         }
                     }
                     if (lds_ld(&sh_abort)) break;
-                    // H - d of the row above -> G' of lane -1: + (i - base)*d
+                    if (tcm) *trace_ext(a, TX_LOAD, sidx) = __builtin_amdgcn_s_memrealtime();
+                    // H - d of the row above -> G' of row -1: + (i - base)*d
                     if (mine) dst[wb] = (int)(uint32_t)pf + (CH * c + wb + 1 - base) * d;
                     if (xsrc && mine && wb < n) a.row0[CH * c + wb] = (int)(uint32_t)pf;
                 }
-                if (chl) {
-                    dst[lane] = (int)pc;
-                    if (c + 1 < NC) pc = s1w[2 * (c + 1) + lane - 8];
+                {
+                    const int k = c - cw;
+                    const int b0 = __builtin_amdgcn_readlane((int)sw, 2 * k), b1 = __builtin_amdgcn_readlane((int)sw, 2 * k + 1);
+                    if (lane == 8) dst[8] = b0;
+                    if (lane == 9) dst[9] = b1;
                 }
+                lds_order();
                 if (lane == 0) lds_publish(&ctr[2], c + 1);
             }
             if (xsrc) xcredit_post(a);
@@ -719,6 +734,11 @@ KernelFn pick_kernel(int W, bool prof, bool sh, bool sd, bool stt) {
     }
 }
 
+// Resident fill workgroups per CU (the grid is at most this many per CU; one
+// granule slot each, + 1).  Every plan that needs more than one WG-stripe per
+// CU runs W >= 8 compute waves (+ loader + publisher), 1-2 workgroups per CU.
+constexpr int kMaxWgPerCu = 4;
+
 // Compute waves per workgroup (+1 loader wave; 16 waves = 1024 threads max).
 const int kWaveChoices[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 15};
 
@@ -761,6 +781,109 @@ TableView view_of(const nw_table* t) {
     v.row_base = (int32_t)t->row_base;
     v.top = t->row_base > 0 ? t->row0 : nullptr;
     return v;
+}
+
+double host_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ---------------------------------------------------------------- Host I/O
+// Streamed slice copies.  A slice of columns [i0, i1)
+// is gathered into dense column blocks of <= kStageBytes by a kernel on the
+// table's stream, alternating between two device staging buffers, while the
+// copy stream DMAs the previous block out: into the destination itself when
+// it is pinned, else into one of two pinned bounce buffers that the host then
+// copies out while the next DMA runs.
+constexpr size_t kStageBytes = (size_t)64 << 20;
+
+void release_io(nw_table* t) {
+    if (t->copy_stream) (void)hipStreamSynchronize(t->copy_stream);
+    for (auto& b : t->d_stage) {
+        (void)hipFree(b);
+        b = nullptr;
+    }
+    for (auto& b : t->h_stage) {
+        if (b) (void)hipHostFree(b);
+        b = nullptr;
+    }
+    t->stage_bytes = 0;
+    for (auto& e : t->cev) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+    }
+    if (t->copy_stream) (void)hipStreamDestroy(t->copy_stream);
+    t->copy_stream = nullptr;
+    if (t->h_seq) (void)hipHostFree(t->h_seq);
+    t->h_seq = nullptr;
+    t->h_seq_bytes = 0;
+}
+
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t at{};
+    const hipError_t e = hipPointerGetAttributes(&at, p);
+    (void)hipGetLastError();            // a pageable pointer is an error here, not a failure
+    return e == hipSuccess && at.type == hipMemoryTypeHost;
+}
+
+template <class Gather>
+int stream_columns(nw_table* t, int64_t i0, int64_t i1, size_t col_bytes, uint8_t* dst, Gather gather,
+                   const char* who) {
+    const double t0 = host_ms();
+    const size_t stage = std::max(kStageBytes, col_bytes);
+    const bool pinned = is_pinned(dst);
+    if (t->stage_bytes < stage || (!pinned && !t->h_stage[0])) {
+        for (auto& b : t->d_stage) {
+            (void)hipFree(b);
+            b = nullptr;
+        }
+        for (auto& b : t->h_stage) {
+            if (b) (void)hipHostFree(b);
+            b = nullptr;
+        }
+        t->stage_bytes = 0;
+        for (auto& b : t->d_stage) NW_HIPCHK(hipMalloc(&b, stage));
+        if (!pinned)
+            for (auto& b : t->h_stage) NW_HIPCHK(hipHostMalloc(&b, stage, hipHostMallocDefault));
+        t->stage_bytes = stage;
+    }
+    if (!t->copy_stream) NW_HIPCHK(hipStreamCreateWithFlags(&t->copy_stream, hipStreamNonBlocking));
+    for (auto& e : t->cev)
+        if (!e) NW_HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    const int64_t per = std::max<int64_t>(1, (int64_t)(t->stage_bytes / col_bytes));
+    const int64_t nb = (i1 - i0 + per - 1) / per;
+    hipEvent_t* gathered = &t->cev[0];
+    hipEvent_t* copied = &t->cev[2];
+    hipError_t e = hipSuccess;
+    auto host_out = [&](int64_t b) {      // bounce path: block b is in h_stage[b & 1]
+        const int64_t c0 = i0 + b * per, c1 = std::min(i1, c0 + per);
+        if (e == hipSuccess) e = hipEventSynchronize(copied[b & 1]);
+        if (e == hipSuccess)
+            std::memcpy(dst + (size_t)(c0 - i0) * col_bytes, t->h_stage[b & 1], (size_t)(c1 - c0) * col_bytes);
+    };
+    for (int64_t b = 0; b < nb && e == hipSuccess; ++b) {
+        const int k = (int)(b & 1);
+        const int64_t c0 = i0 + b * per, c1 = std::min(i1, c0 + per);
+        const size_t bytes = (size_t)(c1 - c0) * col_bytes;
+        if (b >= 2) e = hipStreamWaitEvent(t->stream, copied[k], 0);   // d_stage[k] drained (block b-2)
+        if (e == hipSuccess) {
+            gather(c0, c1, t->d_stage[k]);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipEventRecord(gathered[k], t->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(t->copy_stream, gathered[k], 0);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(pinned ? dst + (size_t)(c0 - i0) * col_bytes : t->h_stage[k], t->d_stage[k], bytes,
+                               hipMemcpyDeviceToHost, t->copy_stream);
+        if (e == hipSuccess) e = hipEventRecord(copied[k], t->copy_stream);
+        if (!pinned && b >= 1) host_out(b - 1);   // overlaps block b's gather + DMA
+    }
+    if (!pinned && nb >= 1 && e == hipSuccess) host_out(nb - 1);
+    if (e == hipSuccess) e = hipStreamSynchronize(t->copy_stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(t->stream);
+    if (e != hipSuccess) return nwi::fail(NW_ERR_HIP, std::string(who) + ": " + hipGetErrorString(e));
+    t->copy_ms = host_ms() - t0;
+    t->copy_bytes = (int64_t)((size_t)(i1 - i0) * col_bytes);
+    return NW_OK;
 }
 
 }  // namespace
@@ -879,7 +1002,10 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         a.credit_want = t->credit_want;
         if (t->xout && (L2 % 64) != 0) return fail(NW_ERR_ARG, "nw_table_fill: a feeding panel needs 64*k rows");
         if (getenv("NW_TRACE")) {
-            const int64_t need = 8 * (int64_t)a.NSW;
+            // header {NSW, stamps after the WG rows}, 8 words per WG-stripe, then
+            // (pair kernel) one mid-table time per 128-row stripe
+            const int64_t nmid = NGk + 4 * (int64_t)plan.NSW;   // + loader (+ pair: per-stripe, publisher) times
+            const int64_t need = 8 + 8 * (int64_t)a.NSW + nmid;
             if (t->trace_n < need) {
                 (void)hipFree(t->trace);
                 t->trace = nullptr;
@@ -888,7 +1014,10 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
                 t->trace_n = need;
             }
             NW_HIPCHK(hipMemsetAsync(t->trace, 0, (size_t)need * 8, t->stream));
-            a.trace = t->trace;
+            t->trace_hdr[0] = (uint64_t)a.NSW;
+            t->trace_hdr[1] = (uint64_t)nmid;
+            NW_HIPCHK(hipMemcpyAsync(t->trace, t->trace_hdr, 16, hipMemcpyHostToDevice, t->stream));
+            a.trace = t->trace + 8;
         }
         int occ = 1;
         const int wgw = W + (skew ? 1 : 2);   // + loader (+ publisher: scan and pair kernels)
@@ -896,11 +1025,25 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         occ = std::max(occ, 1);
         // A panel leaves room on every CU for the kernels of its neighbours
         // and of the transport (RCCL), which its hand-off waits on.
-        const int per_cu = panel ? std::max(1, std::min(2, occ - 1)) : std::min(occ, 16);
+        const int per_cu = panel ? std::max(1, std::min(2, occ - 1)) : std::min(occ, kMaxWgPerCu);
         const int64_t grid = std::min<int64_t>(a.NSW, (int64_t)t->ncu * per_cu);
         a.nslot = (int32_t)std::min<int64_t>(grid + 1, (int64_t)(t->gran_bytes / 8 / a.gpitch));
         if (a.nslot < grid + 1) return fail(NW_ERR_ARG, "nw_table_fill: granule buffer too small");
-        if (a.NSW > 1) NW_HIPCHK(hipMemsetAsync(t->gran, 0, (size_t)a.nslot * a.gpitch * 8, t->stream));
+        // Granule tags carry a 16-bit fill sequence above the WG-stripe index,
+        // so a granule left by an earlier fill never matches and the slots
+        // need clearing (205 MB at 100k^2, inside every timed step before)
+        // only on a fresh buffer, once per 65535 fills, or when the indices
+        // do not fit 16 bits.
+        if (a.NSW > 1) {
+            const size_t used = (size_t)a.nslot * a.gpitch * 8;
+            t->gseq = (t->gseq + 1) & 0xffffu;
+            if (t->gseq == 0 || used > t->gran_clean || a.NSW >= 0x10000) {
+                NW_HIPCHK(hipMemsetAsync(t->gran, 0, used, t->stream));
+                t->gran_clean = std::max(t->gran_clean, used);
+                if (t->gseq == 0) t->gseq = 1;
+            }
+            a.gtag = a.NSW < 0x10000 ? t->gseq << 16 : 0u;
+        }
         NW_HIPCHK(hipEventRecord(t->ev[1], t->stream));
         void* kargs[] = {&a};
         NW_HIPCHK(hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3((unsigned)grid), dim3(64 * wgw), kargs,
@@ -1007,6 +1150,7 @@ void nw_table_destroy(nw_table* t) {
     for (auto& e : t->ev)
         if (e) (void)hipEventDestroy(e);
     if (t->stream) (void)hipStreamDestroy(t->stream);
+    release_io(t);
     delete t;
 }
 
@@ -1065,7 +1209,7 @@ int nw_table_create(int device, int64_t max_L1, int64_t max_L2, uint32_t out_mas
     if ((rc = alloc((void**)&t->row0, (size_t)(max_L1 + 8) * 4))) return bail(rc);
     // Granule slots: one per concurrently running WG-stripe + 1.
     const int64_t gpitch = CH * NC + CH;
-    const int64_t nslot = 16 * (int64_t)t->ncu + 1;
+    const int64_t nslot = kMaxWgPerCu * (int64_t)t->ncu + 1;
     t->gran_bytes = (size_t)(gpitch * nslot * 8);
     if ((rc = alloc((void**)&t->gran, t->gran_bytes))) return bail(rc);
     if ((rc = alloc((void**)&t->ctl, CTL_WORDS * 4))) return bail(rc);
@@ -1076,6 +1220,7 @@ int nw_table_create(int device, int64_t max_L1, int64_t max_L2, uint32_t out_mas
 int nw_table_set_sequences(nw_table* t, const char* s1, int64_t L1, const char* s2, int64_t L2) {
     if (!t || L1 < 0 || L2 < 0 || L1 > t->max_L1 || L2 > t->max_L2 || (L1 && !s1) || (L2 && !s2))
         return fail(NW_ERR_ARG, "nw_table_set_sequences: bad arguments");
+    const double t0 = host_ms();
     HIPCHK(hipSetDevice(t->device));
     t->L1 = L1;
     t->L2 = L2;
@@ -1101,20 +1246,30 @@ int nw_table_set_sequences(nw_table* t, const char* s1, int64_t L1, const char* 
     scan(s1, L1);
     scan(s2, L2);
     t->alpha = (alpha >= 1 && alpha <= 8) ? alpha : 0;
-    std::vector<uint8_t> c1, c2;
-    const void* src1 = s1;
-    const void* src2 = s2;
-    if (t->alpha) {
-        c1.resize((size_t)L1);
-        c2.resize((size_t)L2);
-        for (int64_t i = 0; i < L1; ++i) c1[(size_t)i] = (uint8_t)code[(uint8_t)s1[i]];
-        for (int64_t i = 0; i < L2; ++i) c2[(size_t)i] = (uint8_t)code[(uint8_t)s2[i]];
-        src1 = c1.data();
-        src2 = c2.data();
+    // The (coded) sequences are written straight into pinned staging, so
+    // the upload runs at PCIe rate with no pageable bounce.
+    const size_t need = (size_t)(t->max_L1 + t->max_L2 + 16);
+    if (t->h_seq_bytes < need) {
+        if (t->h_seq) (void)hipHostFree(t->h_seq);
+        t->h_seq = nullptr;
+        t->h_seq_bytes = 0;
+        HIPCHK(hipHostMalloc((void**)&t->h_seq, need, hipHostMallocDefault));
+        t->h_seq_bytes = need;
     }
-    if (L1) HIPCHK(hipMemcpyAsync(t->s1, src1, (size_t)L1, hipMemcpyHostToDevice, t->stream));
-    if (L2) HIPCHK(hipMemcpyAsync(t->s2, src2, (size_t)L2, hipMemcpyHostToDevice, t->stream));
+    uint8_t* h1 = t->h_seq;
+    uint8_t* h2 = t->h_seq + L1;
+    if (t->alpha) {
+        for (int64_t i = 0; i < L1; ++i) h1[i] = (uint8_t)code[(uint8_t)s1[i]];
+        for (int64_t i = 0; i < L2; ++i) h2[i] = (uint8_t)code[(uint8_t)s2[i]];
+    } else {
+        if (L1) std::memcpy(h1, s1, (size_t)L1);
+        if (L2) std::memcpy(h2, s2, (size_t)L2);
+    }
+    if (L1) HIPCHK(hipMemcpyAsync(t->s1, h1, (size_t)L1, hipMemcpyHostToDevice, t->stream));
+    if (L2) HIPCHK(hipMemcpyAsync(t->s2, h2, (size_t)L2, hipMemcpyHostToDevice, t->stream));
     HIPCHK(hipStreamSynchronize(t->stream));
+    t->upload_ms = host_ms() - t0;
+    t->upload_bytes = L1 + L2;
     return NW_OK;
 }
 
@@ -1152,23 +1307,14 @@ int64_t nw_table_score_pitch(const nw_table* t) { return t ? t->spitch : 0; }
 int nw_table_waves(const nw_table* t) { return t ? t->waves : 0; }
 
 static int copy_scores_impl(nw_table* t, int64_t i0, int64_t i1, int32_t* dst) {
-    const int64_t N = t->L2 + 1;
-    // Gather the tiles into dense columns through a bounded staging buffer.
-    const int64_t cols_per = std::max<int64_t>(1, ((int64_t)256 << 20) / (4 * N));
-    int32_t* stage = nullptr;
-    HIPCHK(hipMalloc(&stage, (size_t)(std::min(cols_per, i1 - i0) * N * 4)));
-    hipError_t e = hipSuccess;
-    for (int64_t c0 = i0; c0 < i1 && e == hipSuccess; c0 += cols_per) {
-        const int64_t c1 = std::min(i1, c0 + cols_per);
-        nw_gather_scores_kernel<<<1024, 256, 0, t->stream>>>(view_of(t), (int32_t)t->L2, c0, c1, stage);
-        e = hipGetLastError();
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(dst + (c0 - i0) * N, stage, (size_t)((c1 - c0) * N * 4), hipMemcpyDeviceToHost, t->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(t->stream);
-    }
-    (void)hipFree(stage);
-    if (e != hipSuccess) return fail(NW_ERR_HIP, std::string("nw_table_copy_scores: ") + hipGetErrorString(e));
-    return NW_OK;
+    const TableView v = view_of(t);
+    const int32_t L2 = (int32_t)t->L2;
+    return stream_columns(t, i0, i1, (size_t)(t->L2 + 1) * 4, reinterpret_cast<uint8_t*>(dst),
+                          [&](int64_t c0, int64_t c1, void* buf) {
+                              nw_gather_scores_kernel<<<1024, 256, 0, t->stream>>>(v, L2, c0, c1,
+                                                                                   static_cast<int32_t*>(buf));
+                          },
+                          "nw_table_copy_scores");
 }
 
 int nw_table_copy_scores(nw_table* t, int64_t i0, int64_t i1, int32_t* dst) {
@@ -1212,15 +1358,33 @@ int nw_table_copy_codes(nw_table* t, int64_t i0, int64_t i1, uint8_t* dst) {
     if (i1 > t->L1 + 1) return fail(NW_ERR_ARG, "nw_table_copy_codes: column range");
     if (i1 == i0) return NW_OK;
     HIPCHK(hipSetDevice(t->device));
-    const size_t n = (size_t)((i1 - i0) * (t->L2 + 1));
-    uint8_t* buf = nullptr;
-    HIPCHK(hipMalloc(&buf, n));
-    nw_codes_kernel<<<1024, 256, 0, t->stream>>>(view_of(t), (int32_t)t->L2, i0, i1, buf);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpyAsync(dst, buf, n, hipMemcpyDeviceToHost, t->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(t->stream);
-    (void)hipFree(buf);
-    if (e != hipSuccess) return fail(NW_ERR_HIP, std::string("nw_table_copy_codes: ") + hipGetErrorString(e));
+    const TableView v = view_of(t);
+    const int32_t L2 = (int32_t)t->L2;
+    return stream_columns(t, i0, i1, (size_t)(t->L2 + 1), dst,
+                          [&](int64_t c0, int64_t c1, void* buf) {
+                              nw_codes_kernel<<<1024, 256, 0, t->stream>>>(v, L2, c0, c1, static_cast<uint8_t*>(buf));
+                          },
+                          "nw_table_copy_codes");
+}
+
+int nw_host_alloc(size_t bytes, void** p) {
+    if (!p) return fail(NW_ERR_ARG, "nw_host_alloc: NULL argument");
+    *p = nullptr;
+    hipError_t e = hipHostMalloc(p, std::max<size_t>(bytes, 1), hipHostMallocDefault);
+    if (e != hipSuccess) return fail(NW_ERR_OOM, std::string("nw_host_alloc: ") + hipGetErrorString(e));
+    return NW_OK;
+}
+
+void nw_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int nw_table_io_stats(nw_table* t, double* upload_ms, int64_t* upload_bytes, double* copy_ms, int64_t* copy_bytes) {
+    if (!t) return fail(NW_ERR_ARG, "nw_table_io_stats: NULL table");
+    if (upload_ms) *upload_ms = t->upload_ms;
+    if (upload_bytes) *upload_bytes = t->upload_bytes;
+    if (copy_ms) *copy_ms = t->copy_ms;
+    if (copy_bytes) *copy_bytes = t->copy_bytes;
     return NW_OK;
 }
 

@@ -35,6 +35,7 @@ struct nw_table {
     uint32_t* ctl = nullptr;
     uint64_t* trace = nullptr;      // $NW_TRACE: in-kernel timeline
     int64_t trace_n = 0;
+    uint64_t trace_hdr[2] = {0, 0};
     // Row-panel hand-off (set by nw_panel.hip; all null for a plain table).
     int64_t row_base = 0;           // global row of local row 0
     int64_t L2_total = -1;          // global rows, for the overflow guard (-1: L2)
@@ -43,6 +44,8 @@ struct nw_table {
     uint32_t* xflag = nullptr;      // host-visible block flags, or null
     int64_t xblk = 0;               // chunks per hand-off block
     uint32_t epoch = 0;             // tag of the fill in flight
+    uint32_t gseq = 0;              // WG-stripe granule tag sequence (16 bits, fill_launch)
+    size_t gran_clean = 0;          // bytes of the granule slots zeroed since allocation
     int32_t* row0 = nullptr;        // device: the row above (H - d per column), snapshot by the loader
     uint32_t* xin_credit = nullptr;       // consumer: where it posts "row above read" (FillArgs)
     const uint32_t* xout_credit = nullptr;// producer: its consumer's xin_credit
@@ -62,6 +65,17 @@ struct nw_table {
     float kernel_ms = 0.f, call_ms = 0.f;
     int waves = 0;
     nw_walk_state* walk = nullptr;  // lazily created by the walk services
+    // Host I/O (nw_fill.hip "Host I/O"): pinned upload staging, and the
+    // double-buffered device/pinned staging of streamed slice copies.
+    uint8_t* h_seq = nullptr;       // pinned: coded s1 | s2 for the upload
+    size_t h_seq_bytes = 0;
+    void* d_stage[2] = {nullptr, nullptr};
+    void* h_stage[2] = {nullptr, nullptr};   // pinned bounce buffers (pageable destinations)
+    size_t stage_bytes = 0;
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t cev[4] = {nullptr, nullptr, nullptr, nullptr};   // gathered[2], copied[2]
+    double upload_ms = 0.0, copy_ms = 0.0;
+    int64_t upload_bytes = 0, copy_bytes = 0;
 };
 
 namespace nwi {

@@ -34,7 +34,7 @@ struct FillArgs {
     int64_t spitch;         // 512*NC: elements per 64-row stripe
     uint32_t* D;            // codes: word ((g*NC + q)*64 + lane)
     int32_t* lastcol;       // score-only: H[L1][j] at lastcol[63 + j]
-    uint64_t* gran;         // boundary granules, slot s at gran + s*gpitch
+    uint64_t* gran;         // boundary granules, slot s at gran + s*gpitch (see put_granule)
     int64_t gpitch;
     int32_t nslot;
     uint32_t* ctl;          // CtlWord
@@ -44,6 +44,7 @@ struct FillArgs {
     // row_base+1 .. row_base+L2; row 0 is the boundary row of the panel above.
     int32_t row_base;
     uint32_t epoch;         // tag of this fill's panel hand-off granules
+    uint32_t gtag;          // WG-stripe granule tags of this fill: gtag | (consumer's WG-stripe index)
     const uint64_t* xin;    // top boundary row {epoch, H-d} per column, or null (= seeded row 0)
     uint64_t* xout;         // bottom row granules for the panel below, or null
     uint32_t* xflag;        // host-visible: xflag[b] = epoch once block b of xout is written
@@ -81,6 +82,17 @@ typedef int v2i __attribute__((ext_vector_type(2)));
 
 // Ring slot stride (ints): 8 values of a chunk (+ the scan kernel's 8 top-string bytes).
 constexpr int SLOT = 16;
+
+// WG-stripe to WG-stripe granule: ONE aligned 8-byte write-through (sc1)
+// store {tag, value}; the loader polls it with sc1 loads (R2 of the CDNA
+// guide's Guideline 16: the data is the flag).  Measured at 100k^2: ~1.2 us
+// from the producer wave starting a chunk to its granules stored, ~2.5 us
+// more until the next WG-stripe's loader sees them, wherever the two
+// WG-stripes sit (tools/trace_lag.py; an L2-resident second copy for
+// same-XCD consumers and 128-byte padded lines were both slower).
+__device__ __forceinline__ void put_granule(uint64_t* gout, int64_t idx, uint64_t gr) {
+    __hip_atomic_store(gout + idx, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Hand-off granule load: agent scope between workgroups of one fill, system
 // scope (bypassing L2) for the panel boundary, which another agent writes.
@@ -134,6 +146,24 @@ __device__ __forceinline__ void lds_publish(int* p, int v) {
 // slot reads / writes on their side of the relaxed counter accesses in the
 // instruction stream is all the ordering they need.
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+// Extended trace stamps (tools/trace_lag.py) are compiled in only with
+// -DNW_TRACE_EXT=1 (tools/ab_build.sh): even a never-taken stamp branch in
+// the pair kernel's loops moved the 100k^2 fill by several percent.
+#ifndef NW_TRACE_EXT
+#define NW_TRACE_EXT 0
+#endif
+
+// Trace words after the 8 per WG-stripe (nw_fill.hip, $NW_TRACE; pair kernel):
+// per 128-row stripe the time it starts the middle chunk cm, then per
+// WG-stripe: publisher has stored cm's granules, loader has cm in ring 0,
+// loader reaches cm, loader has a free ring slot for cm.
+enum TraceExt { TX_MID = 0, TX_PUB = 1, TX_LOAD = 2, TX_REACH = 3, TX_CREDIT = 4 };
+__device__ __forceinline__ uint64_t* trace_ext(const FillArgs& a, int kind, int idx) {
+    const int64_t base = 8 * (int64_t)a.NSW;
+    return a.trace + base + (kind == TX_MID ? idx : a.NG + (int64_t)(kind - 1) * a.NSW + idx);
+}
+__device__ __forceinline__ int trace_mid_chunk(int NC, int R) { return ((NC - 1) / 2) & ~(R - 1); }
 
 using KernelFn = void (*)(FillArgs);
 

@@ -141,6 +141,8 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
         if (a.trace && threadIdx.x == 0) {
             a.trace[8 * (int64_t)sidx + 0] = __builtin_amdgcn_s_memrealtime();
             a.trace[8 * (int64_t)sidx + 3] = (uint64_t)blockIdx.x | ((uint64_t)__smid() << 32);
+            if (NW_TRACE_EXT)
+                a.trace[8 * (int64_t)sidx + 7] = (uint64_t)(__builtin_amdgcn_s_getreg(20 | (3 << 11)) & 15);   // XCC_ID
         }
         const int g0 = sidx * a.SQ + min(sidx, a.SR);                 // first pair stripe of the WG-stripe
         const int nw = min(a.SQ + (sidx < a.SR ? 1 : 0), a.NG - g0);
@@ -179,11 +181,10 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                     if (lane < n) {
                         // (plain domain: H - d = G' - 128*nw*d - (i - base)d)
                         const int v = bot[(cd % R) * SLOT + lane] - 128 * nw * d - (CH * cd + lane + 1 - chunk_base(cd)) * d;
-                        const uint64_t tag = publish ? (uint32_t)(sidx + 1) : a.epoch;
+                        const uint64_t tag = publish ? a.gtag | (uint32_t)(sidx + 1) : a.epoch;
                         const uint64_t gr = (tag << 32) | (uint32_t)v;
                         if (publish)
-                            __hip_atomic_store(gout + CH * (int64_t)cd + lane, gr, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
+                            put_granule(gout, CH * (int64_t)cd + lane, gr);
                         else
                             __hip_atomic_store(a.xout + CH * (int64_t)cd + lane, gr, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_SYSTEM);
@@ -197,15 +198,24 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                 }
                 lds_order();
                 if (lane == 0) lds_publish(&ctr[2 * nw + 1], cd);        // those ring slots are free again
+                if (NW_TRACE_EXT && a.trace && lane == 0 && cd > trace_mid_chunk(NC, R) && *trace_ext(a, TX_PUB, sidx) == 0)
+                    *trace_ext(a, TX_PUB, sidx) = __builtin_amdgcn_s_memrealtime();
             }
-        } else         if (loader) {
+        } else if (loader) {
             // ---------------- loader wave: ring 0 (as the one-row kernel's) ----------------
+            // Nothing it waits for per chunk is a fresh global load unless the
+            // granules are not there yet: the granule window (8 chunks, one lane
+            // per granule) and the top-string window (lanes 0..15: the 16 dwords
+            // of those 8 chunks) are prefetched one window ahead; a per-chunk
+            // dependent load made the loader, not the producer, pace every
+            // WG-stripe hop (+11% at 100k^2, tools/trace_lag.py).  Kept inline:
+            // the same loop as a shared __device__ function compiled 5-10%
+            // slower at 100k^2 (profiles/r02_ab_loader.txt).
             const bool seeded = sidx == 0 && !a.xin;
             const bool xsrc = sidx == 0 && a.xin;
             const uint64_t* gin = xsrc ? a.xin : a.gran + (int64_t)(sidx % a.nslot) * a.gpitch;
-            const uint32_t want = xsrc ? a.epoch : (uint32_t)sidx;
+            const uint32_t want = xsrc ? a.epoch : a.gtag | (uint32_t)sidx;
             const uint32_t* s1w = reinterpret_cast<const uint32_t*>(a.s1);
-            const bool chl = lane == 8 || lane == 9;
             const int wk = lane >> 3, wb = lane & 7;
             const int64_t ngr = (int64_t)CH * NC;
             auto gload = [&](int cf) -> uint64_t {
@@ -214,7 +224,12 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
             };
             int cw = 0;
             uint64_t pf = 0, pn = 0;
-            uint32_t pc = chl ? s1w[lane - 8] : 0u;
+            const int64_t nsw = 2 * (int64_t)NC + 16;
+            auto sload = [&](int cf) -> uint32_t {
+                const int64_t x = 2 * (int64_t)cf + lane;
+                return lane < 16 && x < nsw ? s1w[x] : 0u;
+            };
+            uint32_t sw = sload(0), swn = sload(CH);
             if (!seeded) {
                 pf = gload(0);
                 pn = gload(CH);
@@ -224,9 +239,14 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                 if (c == cw + CH) {
                     cw += CH;
                     pf = pn;
+                    sw = swn;
                     if (!seeded) pn = gload(cw + CH);
+                    swn = sload(cw + CH);
                 }
+                const bool tcm = NW_TRACE_EXT && a.trace && lane == 0 && c == trace_mid_chunk(NC, R);
+                if (tcm) *trace_ext(a, TX_REACH, sidx) = __builtin_amdgcn_s_memrealtime();
                 while (lds_ld(&ctr[1]) < c - R + 1) __builtin_amdgcn_s_sleep(1);
+                if (tcm) *trace_ext(a, TX_CREDIT, sidx) = __builtin_amdgcn_s_memrealtime();
                 int* dst = &tring[(c % R) * SLOT];
                 const int base = chunk_base(c);
                 if (seeded) {
@@ -260,13 +280,16 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                         }
                     }
                     if (lds_ld(&sh_abort)) break;
+                    if (tcm) *trace_ext(a, TX_LOAD, sidx) = __builtin_amdgcn_s_memrealtime();
                     // H - d of the row above -> G' of row -1: + (i - base)*d
                     if (mine) dst[wb] = (int)(uint32_t)pf + (CH * c + wb + 1 - base) * d;
                     if (xsrc && mine && wb < n) a.row0[CH * c + wb] = (int)(uint32_t)pf;
                 }
-                if (chl) {
-                    dst[lane] = (int)pc;
-                    if (c + 1 < NC) pc = s1w[2 * (c + 1) + lane - 8];
+                {
+                    const int k = c - cw;
+                    const int b0 = __builtin_amdgcn_readlane((int)sw, 2 * k), b1 = __builtin_amdgcn_readlane((int)sw, 2 * k + 1);
+                    if (lane == 8) dst[8] = b0;
+                    if (lane == 9) dst[9] = b1;
                 }
                 lds_order();
                 if (lane == 0) lds_publish(&ctr[2], c + 1);
@@ -466,6 +489,9 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
             if (nfull > 0) aborted = !wait_slot(0, tA);
             while (c + R <= nfull && !aborted) {
                 rebase(c);
+                // [8*NSW + g]: when this stripe reaches the middle of the table
+                if (NW_TRACE_EXT && a.trace && lane == 0 && c == trace_mid_chunk(NC, R))
+                    *trace_ext(a, TX_MID, g) = __builtin_amdgcn_s_memrealtime();
                 aborted = !full_chunk(c, S0{}, tA, tB) || !full_chunk(c + 1, S1{}, tB, tA) ||
                           !full_chunk(c + 2, S2{}, tA, tB) || !full_chunk(c + 3, S3{}, tB, tA);
                 c += R;

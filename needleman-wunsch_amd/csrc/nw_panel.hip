@@ -185,6 +185,39 @@ double now_ms() {
 
 }  // namespace
 
+// The RCCL transport's callbacks for nw_panel_proxy_run.
+struct RcclProxy {
+    nw_panel* p;
+    nw_table* t;
+    uint32_t epoch;
+    static int recv(void* c, int64_t off, int64_t cnt) {
+        auto* x = static_cast<RcclProxy*>(c);
+        nw_panel* p = x->p;
+        const ncclResult_t r = ncclRecv(p->xin + off, (size_t)cnt, ncclUint64, p->prev, p->comm[(p->pos - 1) & 1],
+                                        p->s_recv);
+        return r == ncclSuccess ? NW_OK : nccl_fail(r, "ncclRecv");
+    }
+    static int flag(void* c, int64_t b, uint64_t spin) {
+        auto* x = static_cast<RcclProxy*>(c);
+        volatile uint32_t* f = x->p->xflag;
+        if (f[b] == x->epoch) return 1;
+        __builtin_ia32_pause();
+        if ((spin & 1023) == 1023 && hipEventQuery(x->t->ev[2]) == hipSuccess) return f[b] == x->epoch ? 1 : -1;
+        return 0;
+    }
+    static int poison(void* c, int64_t off, int64_t cnt) {
+        auto* x = static_cast<RcclProxy*>(c);
+        return nwi::poison(x->p->xout + off, cnt, x->epoch, x->p->s_send);
+    }
+    static int send(void* c, int64_t off, int64_t cnt) {
+        auto* x = static_cast<RcclProxy*>(c);
+        nw_panel* p = x->p;
+        const ncclResult_t r = ncclSend(p->xout + off, (size_t)cnt, ncclUint64, p->next, p->comm[p->pos & 1],
+                                        p->s_send);
+        return r == ncclSuccess ? NW_OK : nccl_fail(r, "ncclSend");
+    }
+};
+
 extern "C" {
 
 int nw_panel_partition(int64_t L2, int nranks, int rank, int64_t* row_base, int64_t* rows) {
@@ -377,6 +410,45 @@ int nw_panel_set_sequences(nw_panel* p, const char* s1, int64_t L1, const char* 
     return NW_OK;
 }
 
+int nw_panel_proxy_run(int64_t L1, int64_t xblk, int has_prev, int has_next, int launched,
+                       const nw_panel_proxy_ops* ops) {
+    if (!ops || L1 < 0 || xblk < 1 || (has_prev && !ops->recv) ||
+        (has_next && (!ops->flag || !ops->send || !ops->poison)))
+        return fail(NW_ERR_ARG, "nw_panel_proxy_run: bad arguments");
+    const int64_t NB = L1 > 0 ? cdiv(cdiv(L1, kChunk), xblk) : 0;
+    auto blk = [&](int64_t b, int64_t* off, int64_t* cnt) {
+        *off = b * xblk * kChunk;
+        *cnt = std::min<int64_t>(xblk * kChunk, L1 - *off);
+    };
+    // 1. every receive before anything is waited for
+    for (int64_t b = 0; has_prev && b < NB; ++b) {
+        int64_t off, cnt;
+        blk(b, &off, &cnt);
+        const int rc = ops->recv(ops->ctx, off, cnt);
+        if (rc) return rc;
+    }
+    // 2. the row below, block by block
+    int rc = NW_OK;
+    bool broken = !launched;
+    for (int64_t b = 0; has_next && b < NB; ++b) {
+        int64_t off, cnt;
+        blk(b, &off, &cnt);
+        for (uint64_t spin = 0; !broken; ++spin) {
+            const int f = ops->flag(ops->ctx, b, spin);
+            if (f > 0) break;
+            if (f < 0) broken = true;   // the kernel ended without this block
+        }
+        if (broken) {
+            const int prc = ops->poison(ops->ctx, off, cnt);
+            if (prc && !rc) rc = prc;
+        }
+        const int src = ops->send(ops->ctx, off, cnt);
+        if (src) return src;
+        if (rc) return rc;
+    }
+    return rc;
+}
+
 int nw_panel_fill(nw_panel* p, int32_t m, int32_t k, int32_t d, uint32_t out_mask) {
     if (!p) return fail(NW_ERR_ARG, "nw_panel_fill: NULL panel");
     if (p->transport == NW_PANEL_GROUP) return fail(NW_ERR_ARG, "nw_panel_fill: group panels use nw_panel_group_fill");
@@ -404,45 +476,11 @@ int nw_panel_fill(nw_panel* p, int32_t m, int32_t k, int32_t d, uint32_t out_mas
     if (rc == NW_OK) rc = post_credit(p, launched && t->xin);
     const int64_t NC = cdiv(p->L1, kChunk);
     const int64_t NB = (p->rows > 0 && p->L1 > 0) ? cdiv(NC, p->xblk) : 0;
-    auto blk = [&](int64_t b, int64_t* off, int64_t* cnt) {
-        *off = b * p->xblk * kChunk;
-        *cnt = std::min<int64_t>(p->xblk * kChunk, p->L1 - *off);
-    };
     int xrc = NW_OK;   // transport failure (reported after the local fill)
     if (p->transport == NW_PANEL_RCCL && NB > 0) {
-        // Every receive is posted before we wait for anything: the panel
-        // above never blocks on us.
-        if (p->prev >= 0) {
-            for (int64_t b = 0; b < NB && !xrc; ++b) {
-                int64_t off, cnt;
-                blk(b, &off, &cnt);
-                ncclResult_t r = ncclRecv(p->xin + off, (size_t)cnt, ncclUint64, p->prev, p->comm[(p->pos - 1) & 1],
-                                          p->s_recv);
-                if (r != ncclSuccess) xrc = nccl_fail(r, "ncclRecv");
-            }
-        }
-        if (p->next >= 0) {
-            bool broken = !launched;
-            volatile uint32_t* flag = p->xflag;
-            for (int64_t b = 0; b < NB && !xrc; ++b) {
-                int64_t off, cnt;
-                blk(b, &off, &cnt);
-                for (uint64_t spin = 0; !broken && flag[b] != epoch; ++spin) {
-                    __builtin_ia32_pause();
-                    if ((spin & 1023) == 1023 && hipEventQuery(t->ev[2]) == hipSuccess) {
-                        broken = flag[b] != epoch;   // kernel ended without this block
-                        break;
-                    }
-                }
-                if (broken) {
-                    const int prc = nwi::poison(p->xout + off, cnt, epoch, p->s_send);
-                    if (prc) xrc = prc;
-                }
-                ncclResult_t r = ncclSend(p->xout + off, (size_t)cnt, ncclUint64, p->next, p->comm[p->pos & 1],
-                                          p->s_send);
-                if (r != ncclSuccess) xrc = nccl_fail(r, "ncclSend");
-            }
-        }
+        RcclProxy px{p, t, epoch};
+        const nw_panel_proxy_ops ops{&px, RcclProxy::recv, RcclProxy::flag, RcclProxy::poison, RcclProxy::send};
+        xrc = nw_panel_proxy_run(p->L1, p->xblk, p->prev >= 0, p->next >= 0, launched, &ops);
     }
     if (launched) rc = nwi::fill_finish(t);
     if (p->transport == NW_PANEL_IPC && rc != NW_OK && p->next >= 0 && p->rows > 0 && p->L1 > 0) {

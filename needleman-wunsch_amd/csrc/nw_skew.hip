@@ -172,7 +172,7 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
             const bool seeded = sidx == 0 && !a.xin;
             const bool xsrc = sidx == 0 && a.xin;
             const uint64_t* gin = xsrc ? a.xin : a.gran + (int64_t)(sidx % a.nslot) * a.gpitch;
-            const uint32_t want = xsrc ? a.epoch : (uint32_t)sidx;
+            const uint32_t want = xsrc ? a.epoch : a.gtag | (uint32_t)sidx;
             const int wk = lane >> 3, wb = lane & 7;   // window copy, byte of the chunk
             // Granule window: lane l holds granule (cw + l/8, column l%8), so
             // one load covers 8 chunks; pn prefetches the next 8.  A poll
@@ -182,9 +182,17 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
                 const int64_t x = (int64_t)CH * cf + lane;
                 return x < ngr ? ld_gran(gin + x, xsrc) : 0ull;
             };
+            // Top-string window (lanes 0..15: the 16 dwords of chunks cw..cw+7),
+            // prefetched one window ahead like the granules: no per-chunk
+            // dependent global load paces the loader (see the pair kernel's loader).
+            const int64_t nsw = 2 * (int64_t)NC1 + 16;
+            auto sload = [&](int cf) -> uint32_t {
+                const int64_t x = 2 * (int64_t)cf + lane;
+                return lane < 16 && x < nsw ? reinterpret_cast<const uint32_t*>(a.s1)[x] : 0u;
+            };
             int cw = 0;
             uint64_t pf = 0, pn = 0;
-            uint8_t pc = a.s1[wb];
+            uint32_t sw = sload(0), swn = sload(CH);
             if (!seeded) {
                 pf = gload(0);
                 pn = gload(CH);
@@ -194,7 +202,9 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
                 if (c == cw + CH) {
                     cw += CH;
                     pf = pn;
+                    sw = swn;
                     if (!seeded) pn = gload(cw + CH);
+                    swn = sload(cw + CH);
                 }
                 while (lds_ld(&ctr[1]) < c - R + 1) __builtin_amdgcn_s_sleep(1);
                 int* dst = &tring[(c % R) * SLOT];
@@ -232,8 +242,10 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
                     if (xsrc && mine && wb < n && CH * c + wb < a.L1) a.row0[CH * c + wb] = (int)(uint32_t)pf;
                 }
                 // window: copy k holds column p + 1 + k at position p
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)sw, 2 * (c - cw));
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)sw, 2 * (c - cw) + 1);
+                const uint8_t pc = (uint8_t)((wb < 4 ? lo : hi) >> (8 * (wb & 3)));
                 swin[wk * SWN + ((CH * c + wb - wk) & (SWN - 1))] = pc;
-                pc = a.s1[CH * (c + 1) + wb];
                 lds_order();
                 if (lane == 0) lds_publish(&ctr[2], c + 9);   // prog = slots done + 8
             }
@@ -305,11 +317,10 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
                 const int n = (q == NC1 - 1) ? nlast : CH;
                 if (lane < n) {
                     const int v = tout[(q & (R - 1)) * SLOT + lane] - d;        // granules carry H - d
-                    const uint64_t tag = publish ? (uint32_t)(sidx + 1) : a.epoch;
+                    const uint64_t tag = publish ? a.gtag | (uint32_t)(sidx + 1) : a.epoch;
                     const uint64_t gr = (tag << 32) | (uint32_t)v;
                     if (publish)
-                        __hip_atomic_store(gout + CH * (int64_t)q + lane, gr, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+                        put_granule(gout, CH * (int64_t)q + lane, gr);
                     else
                         __hip_atomic_store(a.xout + CH * (int64_t)q + lane, gr, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_SYSTEM);

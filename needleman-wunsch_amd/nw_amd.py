@@ -58,11 +58,12 @@ EXPORTS = (
     "nw_table_copy_codes", "nw_table_copy_last_column", "nw_table_score_pitch", "nw_table_waves",
     "nw_table_trace", "nw_table_count_alignments", "nw_table_first_path", "nw_table_walk_elapsed_ms",
     "nw_first_path_banded", "nw_table_hash_columns", "nw_hash_fold",
+    "nw_host_alloc", "nw_host_free", "nw_table_io_stats",
     # include/nw_panel.h
     "nw_panel_partition", "nw_panel_chain", "nw_panel_get_id", "nw_panel_create", "nw_panel_ipc_handle",
     "nw_panel_ipc_connect", "nw_panel_group_create", "nw_panel_destroy", "nw_panel_set_sequences",
     "nw_panel_fill", "nw_panel_group_fill", "nw_panel_stats", "nw_panel_record", "nw_panel_reduce",
-    "nw_panel_rows", "nw_panel_table", "nw_panel_elapsed_ms", "nw_panel_hash_columns",
+    "nw_panel_rows", "nw_panel_table", "nw_panel_elapsed_ms", "nw_panel_hash_columns", "nw_panel_proxy_run",
 )
 
 
@@ -156,8 +157,13 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "nw_table_walk_elapsed_ms": (c_int, [c_p, P(ctypes.c_float), P(ctypes.c_float)]),
         "nw_first_path_banded": (c_int, [c_int, ctypes.c_char_p, c_i64, ctypes.c_char_p, c_i64, c_i32, c_i32, c_i32,
                                          c_i64, c_p, c_i64, P(c_i64)]),
+        "nw_host_alloc": (c_int, [ctypes.c_size_t, P(c_p)]),
+        "nw_host_free": (None, [c_p]),
+        "nw_table_io_stats": (c_int, [c_p, P(ctypes.c_double), P(c_i64), P(ctypes.c_double), P(c_i64)]),
     }
     for name, (res, args) in sigs.items():
+        if os.environ.get("NW_LIB") and not hasattr(lib, name):
+            continue        # an older A/B build (tools/ab_libs.sh) may predate an entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -170,6 +176,38 @@ def _check(rc: int, what: str) -> None:
         lib = load()
         detail = lib.nw_last_error().decode(errors="replace")
         raise NWError(rc, f"{what}: {lib.nw_strerror(rc).decode()}: {detail}")
+
+
+class HostBuffer:
+    """Pinned (page-locked) host memory from nw_host_alloc, viewed as a numpy
+    array: slice copies into it are DMA'd straight from the device."""
+
+    def __init__(self, shape, dtype):
+        lib = load()
+        self.array_dtype = np.dtype(dtype)
+        n = int(np.prod(shape)) * self.array_dtype.itemsize
+        self._p = ctypes.c_void_p()
+        _check(lib.nw_host_alloc(n, ctypes.byref(self._p)), "nw_host_alloc")
+        raw = (ctypes.c_uint8 * max(n, 1)).from_address(self._p.value)
+        self.array = np.frombuffer(raw, dtype=np.uint8, count=n).view(self.array_dtype).reshape(shape)
+
+    def close(self) -> None:
+        if self._p and self._p.value:
+            self.array = None
+            load().nw_host_free(self._p)
+            self._p = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def _bytes(s) -> bytes:
@@ -205,6 +243,14 @@ def unpack_nibbles(nib: np.ndarray, ncell: int) -> np.ndarray:
     out[0::2] = nib & 0xF
     out[1::2] = nib >> 4
     return out[:ncell]
+
+
+def _out(out, shape, dtype):
+    if out is None:
+        return np.empty(shape, dtype=dtype)
+    if out.shape != tuple(shape) or out.dtype != np.dtype(dtype) or not out.flags.c_contiguous:
+        raise ValueError(f"out must be a C-contiguous {np.dtype(dtype)} array of shape {tuple(shape)}")
+    return out
 
 
 class Table:
@@ -275,31 +321,47 @@ class Table:
         _check(self._lib.nw_table_hash_columns(self._h, j0, state[0].ctypes.data, state[1].ctypes.data),
                "nw_table_hash_columns")
 
-    def scores(self, i0: int = 0, i1: int | None = None) -> np.ndarray:
+    def scores(self, i0: int = 0, i1: int | None = None, out: np.ndarray | None = None) -> np.ndarray:
+        """Columns [i0, i1) as int32 (i1-i0, L2+1); `out` (C-contiguous, e.g. a
+        HostBuffer's array) receives them in place."""
         i1 = self.L1 + 1 if i1 is None else i1
-        out = np.empty((i1 - i0, self.L2 + 1), dtype=np.int32)
+        out = _out(out, (i1 - i0, self.L2 + 1), np.int32)
         _check(self._lib.nw_table_copy_scores(self._h, i0, i1, out.ctypes.data), "nw_table_copy_scores")
         return out
 
-    def codes(self, i0: int = 0, i1: int | None = None) -> np.ndarray:
+    def codes(self, i0: int = 0, i1: int | None = None, out: np.ndarray | None = None) -> np.ndarray:
         i1 = self.L1 + 1 if i1 is None else i1
-        out = np.empty((i1 - i0, self.L2 + 1), dtype=np.uint8)
+        out = _out(out, (i1 - i0, self.L2 + 1), np.uint8)
         _check(self._lib.nw_table_copy_codes(self._h, i0, i1, out.ctypes.data), "nw_table_copy_codes")
         return out
+
+    def io_stats(self) -> dict:
+        """Last upload / slice copy: wall ms and bytes (nw_table_io_stats)."""
+        um, cm = ctypes.c_double(), ctypes.c_double()
+        ub, cb = ctypes.c_int64(), ctypes.c_int64()
+        _check(self._lib.nw_table_io_stats(self._h, ctypes.byref(um), ctypes.byref(ub), ctypes.byref(cm),
+                                           ctypes.byref(cb)), "nw_table_io_stats")
+        return {"upload_ms": um.value, "upload_bytes": ub.value, "copy_ms": cm.value, "copy_bytes": cb.value}
 
     def last_column(self) -> np.ndarray:
         out = np.empty(self.L2 + 1, dtype=np.int32)
         _check(self._lib.nw_table_copy_last_column(self._h, out.ctypes.data), "nw_table_copy_last_column")
         return out
 
-    def trace(self) -> np.ndarray:
+    def trace(self, mid: bool = False) -> np.ndarray:
         """In-kernel timeline (needs $NW_TRACE): rows (dequeue, start, end, block|cu<<32,
-        clk_start, clk_end, 0, 0) -- realtime at 100 MHz, clk = shader clock."""
+        clk_start, clk_end, last wave start, 0) per WG-stripe -- realtime at 100 MHz,
+        clk = shader clock.  mid=True: the pair kernel's per-stripe time at the
+        middle chunk of the table instead."""
         n = self._lib.nw_table_trace(self._h, None, 0)
         out = np.zeros(max(n, 0), dtype=np.uint64)
         if n > 0:
             self._lib.nw_table_trace(self._h, out.ctypes.data, n)
-        return out.reshape(-1, 8)
+        if n < 8:
+            return out[:0].reshape(-1, 8) if not mid else out[:0]
+        nsw, nmid = int(out[0]), int(out[1])
+        body = out[8:]
+        return body[8 * nsw:8 * nsw + nmid] if mid else body[:8 * nsw].reshape(-1, 8)
 
     def count_alignments(self) -> int:
         """Number of optimal alignments, mod 2**32 like the reference's counter
@@ -349,6 +411,40 @@ def panel_chain(L2: int, nranks: int, rank: int):
     _check(lib.nw_panel_chain(L2, nranks, rank, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
            "nw_panel_chain")
     return a.value, b.value, c.value
+
+
+_PROXY_RANGE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64)
+_PROXY_FLAG = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64)
+
+
+class _ProxyOps(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("recv", _PROXY_RANGE), ("flag", _PROXY_FLAG),
+                ("poison", _PROXY_RANGE), ("send", _PROXY_RANGE)]
+
+
+def panel_proxy_run(L1: int, xblk: int, has_prev: bool, has_next: bool, launched: bool,
+                    recv=None, flag=None, poison=None, send=None) -> int:
+    """Drive the RCCL transport's host proxy (nw_panel_proxy_run) with Python
+    callbacks: recv/poison/send(off, cnt) -> rc, flag(b, spin) -> 1/0/-1.
+    Returns the proxy's status code."""
+    lib = load()
+    fn = lib.nw_panel_proxy_run
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.POINTER(_ProxyOps)]
+
+    def guard(f, *a):
+        try:
+            return int(f(*a))
+        except Exception:          # a raising callback is a failed transport step
+            return NW_ERR_STATE
+
+    def rng(f):
+        return _PROXY_RANGE(lambda _c, off, cnt: guard(f, off, cnt) if f else NW_ERR_ARG)
+
+    ops = _ProxyOps(None, rng(recv), _PROXY_FLAG(lambda _c, b, spin: guard(flag, b, spin) if flag else -1),
+                    rng(poison), rng(send))
+    return fn(L1, xblk, int(has_prev), int(has_next), int(launched), ctypes.byref(ops))
 
 
 def panel_get_id() -> bytes:

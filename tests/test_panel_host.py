@@ -176,3 +176,141 @@ def test_gloo_two_ranks_chain(tmp_path, L1, L2):
     assert tuple(int(x) for x in z["stats"]) == st
     assert float(z["slowest"]) == 2.0
     np.testing.assert_array_equal(z["table"], H[:, 1:])
+
+
+# ------------------------------------------- RCCL host proxy (sequencing only)
+POISON = 0x80000000
+
+
+def _blocks(L1, xblk):
+    step = 8 * xblk
+    return [(off, min(step, L1 - off)) for off in range(0, L1, step)]
+
+
+@pytest.mark.parametrize("L1,xblk", [(1, 1), (64, 1), (65, 1), (1000, 4), (100_000, 512)])
+def test_proxy_posts_every_recv_first_then_sends_in_order(L1, xblk):
+    log = []
+    rc = nw_amd.panel_proxy_run(L1, xblk, True, True, True,
+                                recv=lambda o, c: log.append(("recv", o, c)) or 0,
+                                flag=lambda b, spin: 1 if spin >= 2 else 0,
+                                poison=lambda o, c: log.append(("poison", o, c)) or 0,
+                                send=lambda o, c: log.append(("send", o, c)) or 0)
+    assert rc == 0
+    blocks = _blocks(L1, xblk)
+    assert log == [("recv", o, c) for o, c in blocks] + [("send", o, c) for o, c in blocks]
+
+
+def test_proxy_poisons_what_the_kernel_never_produced():
+    L1, xblk, dead = 1000, 2, 5          # the producer kernel ends after block 4
+    log = []
+    rc = nw_amd.panel_proxy_run(L1, xblk, False, True, True,
+                                flag=lambda b, spin: 1 if b < dead else (-1 if spin > 3 else 0),
+                                poison=lambda o, c: log.append(("poison", o, c)) or 0,
+                                send=lambda o, c: log.append(("send", o, c)) or 0)
+    assert rc == 0
+    want = []
+    for b, (o, c) in enumerate(_blocks(L1, xblk)):
+        if b >= dead:
+            want.append(("poison", o, c))
+        want.append(("send", o, c))
+    assert log == want
+
+
+def test_proxy_unlaunched_kernel_poisons_every_block_without_polling():
+    log = []
+    rc = nw_amd.panel_proxy_run(100, 1, False, True, False, flag=lambda b, s: pytest.fail("polled"),
+                                poison=lambda o, c: log.append("p") or 0, send=lambda o, c: log.append("s") or 0)
+    assert rc == 0 and log == ["p", "s"] * len(_blocks(100, 1))
+
+
+def test_proxy_stops_at_the_first_transport_failure():
+    sent = []
+    rc = nw_amd.panel_proxy_run(640, 8, False, True, True, flag=lambda b, s: 1, poison=lambda o, c: 0,
+                                send=lambda o, c: (sent.append(o), nw_amd.NW_ERR_HIP if o == 128 else 0)[1])
+    assert rc == nw_amd.NW_ERR_HIP and sent == [0, 64, 128]
+    posted = []
+    rc = nw_amd.panel_proxy_run(640, 8, True, True, True,
+                                recv=lambda o, c: (posted.append(o), nw_amd.NW_ERR_HIP if o == 64 else 0)[1],
+                                flag=lambda b, s: pytest.fail("no send after a failed recv"))
+    assert rc == nw_amd.NW_ERR_HIP and posted == [0, 64]
+    # a poison failure is reported after its block went out
+    log = []
+    rc = nw_amd.panel_proxy_run(200, 8, False, True, False, poison=lambda o, c: nw_amd.NW_ERR_HIP,
+                                send=lambda o, c: log.append(o) or 0)
+    assert rc == nw_amd.NW_ERR_HIP and log == [0]
+
+
+def test_proxy_rejects_missing_callbacks():
+    assert nw_amd.panel_proxy_run(64, 0, False, True, True, flag=lambda b, s: 1) == nw_amd.NW_ERR_ARG
+    assert nw_amd.panel_proxy_run(-1, 1, False, False, True) == nw_amd.NW_ERR_ARG
+
+
+def _proxy_worker(rank, world, port, L1, L2, mkd, dead, out_path):
+    """Two ranks exchange one boundary row through nw_panel_proxy_run with
+    gloo point-to-point in the role of ncclSend / ncclRecv: granules
+    {epoch, H - d} per column, blocks of 8*xblk, receives posted up front."""
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m, k, d = mkd
+    epoch, xblk = 7, 3
+    s1, s2 = O.gen_dna(1, L1), O.gen_dna(2, L2)
+    base, rows = nw_amd.panel_partition(L2, world, rank)
+    prev, nxt, _ = nw_amd.panel_chain(L2, world, rank)
+    works = []
+    if rank == 0:
+        Hb, _, _ = O.fill_band(s1, s2[base:base + rows], base, _seed_row(L1, d), m, k, d)
+        vals = (Hb[1:, -1].astype(np.int64) - d) & 0xFFFFFFFF
+        xout = torch.from_numpy(((epoch << 32) | vals).astype(np.int64))
+
+        def poison(o, c):
+            xout[o:o + c] = ((epoch | POISON) << 32) - (1 << 64)   # as int64
+            return 0
+        rc = nw_amd.panel_proxy_run(L1, xblk, prev >= 0, nxt >= 0, True,
+                                    flag=lambda b, spin: 1 if b < dead else -1, poison=poison,
+                                    send=lambda o, c: works.append(dist.isend(xout[o:o + c].clone(), dst=nxt)) or 0)
+    else:
+        xin = torch.zeros(L1, dtype=torch.int64)
+        slices = []
+
+        def recv(o, c):
+            buf = torch.zeros(c, dtype=torch.int64)
+            slices.append((o, buf))
+            works.append(dist.irecv(buf, src=prev))
+            return 0
+        rc = nw_amd.panel_proxy_run(L1, xblk, prev >= 0, nxt >= 0, True, recv=recv)
+    for w in works:
+        w.wait()
+    if rank == 1:
+        for o, buf in slices:
+            xin[o:o + buf.numel()] = buf
+        g = xin.numpy().astype(np.uint64)
+        np.savez(out_path, rc=rc, tags=(g >> np.uint64(32)).astype(np.int64),
+                 vals=(g & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dead", [10**9, 4])
+def test_gloo_two_ranks_proxy_moves_the_boundary_row(tmp_path, dead):
+    import torch.multiprocessing as mp
+    L1, L2, mkd = 500, 300, (2, 3, 5)
+    out = str(tmp_path / "r1.npz")
+    mp.spawn(_proxy_worker, args=(2, _free_port(), L1, L2, mkd, dead, out), nprocs=2, join=True)
+    z = np.load(out)
+    assert int(z["rc"]) == 0
+    s1, s2 = O.gen_dna(1, L1), O.gen_dna(2, L2)
+    H, _, _ = O.fill(s1, s2, *mkd)
+    base, rows = nw_amd.panel_partition(L2, 2, 1)
+    nblk_ok = min(dead, len(_blocks(L1, 3)))
+    ok = min(L1, nblk_ok * 24)
+    assert (z["tags"][:ok] == 7).all()
+    assert (z["tags"][ok:] == (7 | POISON)).all()
+    # the delivered granules are the row above panel 1 (H - d), and filling
+    # panel 1 from them gives the whole table's rows
+    np.testing.assert_array_equal(z["vals"][:ok], H[1:ok + 1, base] - mkd[2])
+    if ok == L1:
+        top = np.concatenate([[H[0, base]], z["vals"] + mkd[2]]).astype(np.int32)
+        Hb, _, _ = O.fill_band(s1, s2[base:], base, top, *mkd)
+        np.testing.assert_array_equal(Hb, H[:, base:])

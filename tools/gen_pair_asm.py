@@ -37,6 +37,7 @@ import os
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 OUT = os.path.join(ROOT, "needleman-wunsch_amd", "csrc", "nw_pair_chunk.inc")
 READ_AT = 6            # step whose gaps issue the next slot's progress and data reads
+ALIGN = None           # None, or the byte phase (0 / 4) mod 8 at which every block starts
 
 
 def GA(s):
@@ -212,6 +213,11 @@ def block(ST, P, HH=True, FF=True):
         emit(It("", "v_xor_b32_e32 %[accB], 0xffffff, %[accB]"))
     emit(It("PW", "ds_write_b32 %[cb], %[cv] offset:16", lds=True))         # prog[w+1] = c+1
     lines = [it.text for it in out]
+    if ALIGN is not None:
+        # start the block at a fixed place in a 64-byte line (MI355X_MICROARCH.md,
+        # "Code-placement sensitivity"), jumping over the padding: the block's
+        # own layout no longer depends on the compiler's code around it
+        lines = ["s_branch 1f", ".p2align 6", "1:"] + (["s_nop 0"] if ALIGN == 4 else []) + lines
     last = max(i for i, x in enumerate(lines) if x.startswith("ds_read"))
     k = sum(1 for x in lines[last + 1:] if x.startswith("ds_"))
     lines.append(f"s_waitcnt lgkmcnt({min(k, 15)})")
@@ -280,8 +286,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=OUT)
     ap.add_argument("--read-at", type=int, default=READ_AT)
+    ap.add_argument("--align", type=int, choices=(0, 4), default=ALIGN)
     args = ap.parse_args()
     globals()["READ_AT"] = args.read_at
+    globals()["ALIGN"] = args.align
     parts = ["// GENERATED by tools/gen_pair_asm.py -- do not edit; see the generator for the schedule.\n",
              OPERANDS,
              "template <bool HH, bool FF, bool ST, bool P>\n"
