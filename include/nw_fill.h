@@ -195,6 +195,25 @@ int nw_table_count_alignments(nw_table *t, uint32_t *count);
  * 2 = up (gap over s2[j]), 4 = left (s1[i] over a gap).  cap >= L1 + L2. */
 int nw_table_first_path(nw_table *t, uint8_t *moves, int64_t cap, int64_t *n);
 
+/* nw_table_enumerate_paths: every optimal alignment, in the order the
+ * reference prints them, each computed independently on the device (the
+ * reference's "parallel traceback" future work, README:195-200).  The
+ * reference prints in the order of its depth-first walk, which tries diag,
+ * then left, then up at every cell (needleman-wunsch.c:209-331).  With
+ * C(i,j) = the number of code paths from (i,j) to (0,0) (a saturating
+ * uint64 table on the device, cap 2^62), alignment k of that order is
+ * unranked from the corner in O(L1 + L2): diag if k < C(diag cell), else
+ * k -= C(diag cell) and try left, then up -- one thread per alignment.
+ * Alignments first .. first+count-1: alignment first+p goes to
+ * moves[p*stride ..] as its moves from (L1,L2) back to (0,0) -- the order the
+ * reference fills its X / Y buffers -- 1 = diag, 2 = up, 4 = left, and
+ * lens[p] = its length (0 past the last one).  stride >= L1 + L2.  *n (nullable)
+ * = alignments written; *total (nullable) = alignments in all, saturated at
+ * 2^62 (0 for two empty strings, whose walk prints nothing).  Device memory:
+ * 8 bytes per cell for C, computed once per fill. */
+int nw_table_enumerate_paths(nw_table *t, uint64_t first, uint64_t count, uint8_t *moves,
+                             int64_t stride, int32_t *lens, uint64_t *n, uint64_t *total);
+
 /* nw_first_path_banded: nw_table_first_path's result without the full
  * table, for pairs whose direction codes do not fit (or are not wanted) in
  * device memory: a score-only forward pass keeps one boundary row per band of

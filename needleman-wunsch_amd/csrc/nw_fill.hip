@@ -587,58 +587,6 @@ __global__ void nw_poison_kernel(uint64_t* p, int64_t n, uint32_t epoch) {
         __hip_atomic_store(p + x, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Device view of a filled table for the copy / hash kernels.
-struct TableView {
-    const int32_t* tiles;   // score tiles
-    int64_t spitch;
-    const uint32_t* D;      // codes, or null
-    int32_t NC;             // chunks per stripe of the layout (scan: ceil(L1/8); skew: ceil((L1+63)/8))
-    int32_t skew;           // 1: skewed layout (nw_skew.hip), 0: column layout (scan kernel)
-    int32_t pair;           // 1: column layout with rows permuted (nw_pair.hip)
-    int32_t d;
-    int32_t row_base;       // panels: global row of local row 0
-    const int32_t* top;     // panels: the row above (H - d, nw_table.row0), or null for row 0 = seed
-};
-
-// Score of cell (i, j) in the device layout.  Row 0 and column 0 are the
-// reference's seeds (computation.c:93-120), computed, not stored; a panel's
-// row 0 is the last row of the panel above, kept in row0 by the loader.
-// Interior cells live in stripe tiles: stripe g = (j-1)/64, lane l =
-// (j-1)%64, spitch = 512*NC elements per stripe.  Quad tiles (NW_SCORE_X4):
-// column i = 4q + r + 1 at g*spitch + (q*64 + l)*4 + r, so a lane's 4
-// consecutive columns are one 16-byte store and a chunk is 2 KB contiguous.
-// Column tiles: g*spitch + (i-1)*64 + l, one 256-byte store per column.
-// Skewed layout (nw_skew.inc): stored by step t = c + (r & 63) instead of
-// by column, same quad tiles.
-// Pair layout (nw_pair.hip): the column layout of the permuted row
-// nwi::pair_row(r).
-__host__ __device__ __forceinline__ int64_t score_index(int64_t r, int64_t c, int64_t spitch, bool skew = false,
-                                                         bool pair = false) {
-    if (pair) r = nwi::pair_row(r);
-    if (skew) c += r & 63;
-#if NW_SCORE_X4
-    return (r >> 6) * spitch + ((c >> 2) * 64 + (r & 63)) * 4 + (c & 3);
-#else
-    return (r >> 6) * spitch + c * 64 + (r & 63);
-#endif
-}
-
-// Code word and bit position of interior cell (i, j) (see include/nw_fill.h).
-__host__ __device__ __forceinline__ int64_t code_word(int64_t i, int64_t j, int64_t NC, bool skew, int* shift,
-                                                      bool pair = false) {
-    const int64_t rr = pair ? nwi::pair_row(j - 1) : j - 1;
-    const int64_t g = rr >> 6, l = rr & 63;
-    const int64_t t = (i - 1) + (skew ? l : 0);
-    *shift = 21 - 3 * (int)(t & 7);
-    return (g * (NC + 1) + (t >> 3) + 1) * 64 + l;
-}
-
-__device__ __forceinline__ int32_t score_at(const TableView& v, int64_t i, int64_t j) {
-    if (i == 0) return (int32_t)(-(j + v.row_base) * (int64_t)v.d);
-    if (j == 0) return v.top ? v.top[i - 1] + v.d : (int32_t)(-i * (int64_t)v.d);
-    return v.tiles[score_index(j - 1, i - 1, v.spitch, v.skew, v.pair)];
-}
-
 // Dense i-major copy of columns [i0, i1): out[(i-i0)*(L2+1) + j].
 __global__ void nw_gather_scores_kernel(TableView v, int32_t L2, int64_t i0, int64_t i1, int32_t* out) {
     const int64_t N = (int64_t)L2 + 1;
@@ -646,17 +594,6 @@ __global__ void nw_gather_scores_kernel(TableView v, int32_t L2, int64_t i0, int
     for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n;
          x += (int64_t)gridDim.x * blockDim.x)
         out[x] = score_at(v, i0 + x / N, x % N);
-}
-
-// Direction code of cell (i, j).  A panel's row 0 belongs to the panel above
-// and reads as 0 here.
-__device__ __forceinline__ uint32_t code_at(const TableView& v, int64_t i, int64_t j) {
-    if (j == 0 && v.row_base > 0) return 0u;
-    if (i == 0) return j == 0 ? 0u : 2u;          // (0,0): none; (0,j): up
-    if (j == 0) return 4u;                         // (i,0): left
-    int sh;
-    const int64_t wd = code_word(i, j, v.NC, v.skew, &sh, v.pair);
-    return (v.D[wd] >> sh) & 7u;
 }
 
 // Dense nibble packing for nw_fill(): byte b = code(2b) | code(2b+1) << 4.
@@ -769,19 +706,6 @@ StripePlan plan_stripes(int64_t NG, int ncu, int wmax = 15) {
     return p;
 }
 
-TableView view_of(const nw_table* t) {
-    TableView v{};
-    v.tiles = t->H;
-    v.spitch = t->spitch;
-    v.D = (t->last_mask & NW_OUT_DIRS) ? t->D : nullptr;
-    v.NC = (int32_t)t->lay_NC;
-    v.skew = t->skew;
-    v.pair = t->pair;
-    v.d = t->last_d;
-    v.row_base = (int32_t)t->row_base;
-    v.top = t->row_base > 0 ? t->row0 : nullptr;
-    return v;
-}
 
 double host_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -887,6 +811,24 @@ int stream_columns(nw_table* t, int64_t i0, int64_t i1, size_t col_bytes, uint8_
 }
 
 }  // namespace
+
+namespace nwk {
+
+TableView view_of(const nw_table* t) {
+    TableView v{};
+    v.tiles = t->H;
+    v.spitch = t->spitch;
+    v.D = (t->last_mask & NW_OUT_DIRS) ? t->D : nullptr;
+    v.NC = (int32_t)t->lay_NC;
+    v.skew = t->skew;
+    v.pair = t->pair;
+    v.d = t->last_d;
+    v.row_base = (int32_t)t->row_base;
+    v.top = t->row_base > 0 ? t->row0 : nullptr;
+    return v;
+}
+
+}  // namespace nwk
 
 namespace nwi {
 
@@ -1100,6 +1042,7 @@ int fill_finish(nw_table* t) {
     t->stats.greatest_abs_interior = stt ? (int32_t)ctl[CTL_GAV] : 0;
     t->stats.branch_count = stt ? ctl[CTL_BC] : 0u;
     t->filled = true;
+    ++t->fill_serial;
     t->last_mask = t->pend_mask;
     t->last_d = d;
     t->waves = t->pend_W;

@@ -59,6 +59,7 @@ struct nw_table {
     int pend_pair = 0;
     // results of the last fill
     bool filled = false;
+    uint64_t fill_serial = 0;       // completed fills (walk services cache per fill)
     uint32_t last_mask = 0;
     int32_t last_d = 0;
     nw_stats stats{};

@@ -165,6 +165,79 @@ __device__ __forceinline__ uint64_t* trace_ext(const FillArgs& a, int kind, int 
 }
 __device__ __forceinline__ int trace_mid_chunk(int NC, int R) { return ((NC - 1) / 2) & ~(R - 1); }
 
+// ---------------------------------------------------------------- table views
+// (shared by the copy / hash kernels of nw_fill.hip and the walk services of
+// nw_walk.hip)
+#ifndef NW_SCORE_X4
+#define NW_SCORE_X4 1
+#endif
+
+// Device view of a filled table for the copy / hash kernels.
+struct TableView {
+    const int32_t* tiles;   // score tiles
+    int64_t spitch;
+    const uint32_t* D;      // codes, or null
+    int32_t NC;             // chunks per stripe of the layout (scan: ceil(L1/8); skew: ceil((L1+63)/8))
+    int32_t skew;           // 1: skewed layout (nw_skew.hip), 0: column layout (scan kernel)
+    int32_t pair;           // 1: column layout with rows permuted (nw_pair.hip)
+    int32_t d;
+    int32_t row_base;       // panels: global row of local row 0
+    const int32_t* top;     // panels: the row above (H - d, nw_table.row0), or null for row 0 = seed
+};
+
+// Score of cell (i, j) in the device layout.  Row 0 and column 0 are the
+// reference's seeds (computation.c:93-120), computed, not stored; a panel's
+// row 0 is the last row of the panel above, kept in row0 by the loader.
+// Interior cells live in stripe tiles: stripe g = (j-1)/64, lane l =
+// (j-1)%64, spitch = 512*NC elements per stripe.  Quad tiles (NW_SCORE_X4):
+// column i = 4q + r + 1 at g*spitch + (q*64 + l)*4 + r, so a lane's 4
+// consecutive columns are one 16-byte store and a chunk is 2 KB contiguous.
+// Column tiles: g*spitch + (i-1)*64 + l, one 256-byte store per column.
+// Skewed layout (nw_skew.inc): stored by step t = c + (r & 63) instead of
+// by column, same quad tiles.
+// Pair layout (nw_pair.hip): the column layout of the permuted row
+// nwi::pair_row(r).
+__host__ __device__ __forceinline__ int64_t score_index(int64_t r, int64_t c, int64_t spitch, bool skew = false,
+                                                         bool pair = false) {
+    if (pair) r = nwi::pair_row(r);
+    if (skew) c += r & 63;
+#if NW_SCORE_X4
+    return (r >> 6) * spitch + ((c >> 2) * 64 + (r & 63)) * 4 + (c & 3);
+#else
+    return (r >> 6) * spitch + c * 64 + (r & 63);
+#endif
+}
+
+// Code word and bit position of interior cell (i, j) (see include/nw_fill.h).
+__host__ __device__ __forceinline__ int64_t code_word(int64_t i, int64_t j, int64_t NC, bool skew, int* shift,
+                                                      bool pair = false) {
+    const int64_t rr = pair ? nwi::pair_row(j - 1) : j - 1;
+    const int64_t g = rr >> 6, l = rr & 63;
+    const int64_t t = (i - 1) + (skew ? l : 0);
+    *shift = 21 - 3 * (int)(t & 7);
+    return (g * (NC + 1) + (t >> 3) + 1) * 64 + l;
+}
+
+__device__ __forceinline__ int32_t score_at(const TableView& v, int64_t i, int64_t j) {
+    if (i == 0) return (int32_t)(-(j + v.row_base) * (int64_t)v.d);
+    if (j == 0) return v.top ? v.top[i - 1] + v.d : (int32_t)(-i * (int64_t)v.d);
+    return v.tiles[score_index(j - 1, i - 1, v.spitch, v.skew, v.pair)];
+}
+
+// Direction code of cell (i, j).  A panel's row 0 belongs to the panel above
+// and reads as 0 here.
+__device__ __forceinline__ uint32_t code_at(const TableView& v, int64_t i, int64_t j) {
+    if (j == 0 && v.row_base > 0) return 0u;
+    if (i == 0) return j == 0 ? 0u : 2u;          // (0,0): none; (0,j): up
+    if (j == 0) return 4u;                         // (i,0): left
+    int sh;
+    const int64_t wd = code_word(i, j, v.NC, v.skew, &sh, v.pair);
+    return (v.D[wd] >> sh) & 7u;
+}
+
+// The device view of a table's last fill (nw_fill.hip).
+TableView view_of(const nw_table* t);
+
 using KernelFn = void (*)(FillArgs);
 
 // nw_skew.hip: the skewed-stripe kernel for W compute waves per workgroup

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "nw_internal.h"
+#include "nw_kern.h"
 
 struct nw_walk_state {
     uint64_t* rows = nullptr;     // count hand-off granules {tag, P}, (NG-1) x L1
@@ -37,6 +38,12 @@ struct nw_walk_state {
     uint32_t* ctl = nullptr;      // [0] dequeue, [1] abort, [2] result, [3] path length lo, [4] hi / error
     uint8_t* moves = nullptr;     // first path, back to front
     size_t moves_bytes = 0;
+    uint64_t* cnt = nullptr;      // enumeration: saturating path counts, i-major (L1+1)*(L2+1)
+    size_t cnt_bytes = 0;
+    uint64_t cnt_serial = 0;      // fill_serial the counts belong to (0: none)
+    uint8_t* emoves = nullptr;    // enumeration batch: moves and lengths
+    int32_t* elens = nullptr;
+    size_t ebytes = 0, elens_n = 0;
     float count_ms = 0.f, path_ms = 0.f;
 };
 
@@ -215,6 +222,110 @@ __global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, in
     }
 }
 
+// ---------------------------------------------------------------- enumeration
+// Every optimal alignment, in the reference's print order, each one computed
+// on its own (the reference's "parallel traceback" future work, README:195-200).
+// The reference prints alignments in the order of its depth-first walk, which
+// tries diag, then left, then up at every cell (needleman-wunsch.c:296-322).
+// With C(i,j) = the number of code paths from (i,j) to (0,0), alignment k
+// (0-based, in that order) is found by walking from the corner: take diag if
+// k < C(diag cell), else k -= C(diag cell) and try left, then up.  So a
+// thread per alignment writes its moves independently; C is a saturating
+// uint64 (cap 2^62: every k below the cap is unranked exactly).
+constexpr uint64_t CNT_CAP = 1ull << 62;
+constexpr int CT = 64;      // count tile: CT columns x 64 rows
+
+__device__ __forceinline__ uint64_t sat_add(uint64_t a, uint64_t b) {
+    const uint64_t s = a + b;              // a, b <= CNT_CAP: no wrap
+    return s < CNT_CAP ? s : CNT_CAP;
+}
+
+// Row 0 and column 0: one path each (left / up codes, computation.c:102-120).
+__global__ void nw_count_border_kernel(uint64_t* cnt, int64_t L1, int64_t L2) {
+    const int64_t N = L2 + 1;
+    for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x <= L1 + L2;
+         x += (int64_t)gridDim.x * blockDim.x) {
+        if (x <= L2) cnt[x] = 1;                       // (0, j)
+        else cnt[(x - L2) * N] = 1;                    // (i, 0)
+    }
+}
+
+// One 64-row x CT-column tile per workgroup (a wave, lane = row), tiles of one
+// tile anti-diagonal per launch.  The tile is swept in anti-diagonal order
+// through LDS: cell (i, j) needs (i-1, j), (i, j-1), (i-1, j-1), all written
+// by an earlier step or read into the halo (row j0-1, column i0-1).
+__global__ __launch_bounds__(64) void nw_count_tiles_kernel(nwk::TableView v, uint64_t* cnt, int64_t L1, int64_t L2,
+                                                            int diag, int ntj) {
+    __shared__ uint64_t T[CT + 1][64 + 1];          // [column - i0 + 1][row - j0 + 1]
+    const int lane = threadIdx.x;
+    const int bj = max(0, diag - (int)((L1 + CT - 1) / CT - 1)) + (int)blockIdx.x;
+    const int bi = diag - bj;
+    if (bj >= ntj || bi < 0) return;
+    const int64_t N = L2 + 1;
+    const int64_t i0 = 1 + (int64_t)CT * bi, j0 = 1 + 64 * (int64_t)bj;
+    const int64_t j = j0 + lane;
+    // halo: row j0-1 over columns i0-1 .. i0+CT-1, column i0-1 over the tile's rows
+    for (int c = lane; c <= CT; c += 64) {
+        const int64_t i = i0 - 1 + c;
+        T[c][0] = i <= L1 ? cnt[i * N + (j0 - 1)] : 0;
+    }
+    T[0][lane + 1] = j <= L2 ? cnt[(i0 - 1) * N + j] : 0;
+    __syncthreads();
+    for (int t = 0; t < CT + 63; ++t) {
+        const int c = t - lane;                     // this lane's column in the tile
+        const int64_t i = i0 + c;
+        if (c >= 0 && c < CT && i <= L1 && j <= L2) {
+            const uint32_t code = nwk::code_at(v, i, j);
+            uint64_t x = 0;
+            if (code & 1u) x = T[c][lane];                       // diag (i-1, j-1)
+            if (code & 4u) x = sat_add(x, T[c][lane + 1]);       // left (i-1, j)
+            if (code & 2u) x = sat_add(x, T[c + 1][lane]);       // up   (i, j-1)
+            T[c + 1][lane + 1] = x;
+        }
+        __syncthreads();
+    }
+    for (int c = 0; c < CT; ++c) {
+        const int64_t i = i0 + c;
+        if (i <= L1 && j <= L2) cnt[i * N + j] = T[c + 1][lane + 1];
+    }
+}
+
+// Alignment first + p for p = 0 .. count-1: its moves from the corner back to
+// (0,0) -- the order the reference fills its X / Y buffers -- 1 = diag,
+// 2 = up, 4 = left; lens[p] = number of moves (0 if there is no such path).
+__global__ void nw_unrank_kernel(nwk::TableView v, const uint64_t* cnt, int64_t L1, int64_t L2, uint64_t first,
+                                 uint64_t count, uint64_t total, uint8_t* moves, int64_t stride, int32_t* lens) {
+    const int64_t N = L2 + 1;
+    for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < count;
+         p += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t k = first + p;
+        uint8_t* out = moves + p * (uint64_t)stride;
+        if (k >= total) {
+            lens[p] = 0;
+            continue;
+        }
+        int64_t i = L1, j = L2, n = 0;
+        while (i > 0 || j > 0) {
+            const uint32_t code = i == 0 ? 2u : (j == 0 ? 4u : nwk::code_at(v, i, j));
+            uint8_t mv = 2;
+            if (code & 1u) {
+                const uint64_t c = cnt[(i - 1) * N + (j - 1)];
+                if (k < c) mv = 1;
+                else k -= c;
+            }
+            if (mv != 1 && (code & 4u)) {
+                const uint64_t c = cnt[(i - 1) * N + j];
+                if (k < c) mv = 4;
+                else k -= c;
+            }
+            out[n++] = mv;
+            if (mv != 4) --j;
+            if (mv != 2) --i;
+        }
+        lens[p] = (int32_t)n;
+    }
+}
+
 int check_walkable(nw_table* t, const char* who) {
     if (!t) return nwi::fail(NW_ERR_ARG, std::string(who) + ": NULL table");
     if (!t->filled || !(t->last_mask & NW_OUT_DIRS))
@@ -242,6 +353,9 @@ void walk_release(nw_table* t) {
     (void)hipFree(t->walk->rows);
     (void)hipFree(t->walk->ctl);
     (void)hipFree(t->walk->moves);
+    (void)hipFree(t->walk->cnt);
+    (void)hipFree(t->walk->emoves);
+    (void)hipFree(t->walk->elens);
     delete t->walk;
     t->walk = nullptr;
 }
@@ -450,6 +564,76 @@ int nw_first_path_banded(int device, const char* s1, int64_t L1, const char* s2,
     std::reverse_copy(path.begin(), path.end(), moves);
     *n = (int64_t)path.size();
     return done(NW_OK);
+}
+
+
+int nw_table_enumerate_paths(nw_table* t, uint64_t first, uint64_t count, uint8_t* moves, int64_t stride,
+                             int32_t* lens, uint64_t* n_out, uint64_t* total) {
+    int rc = check_walkable(t, "nw_table_enumerate_paths");
+    if (rc) return rc;
+    const int64_t L1 = t->L1, L2 = t->L2;
+    if ((count && (!moves || !lens)) || stride < L1 + L2)
+        return nwi::fail(NW_ERR_ARG, "nw_table_enumerate_paths: bad arguments (stride >= L1 + L2)");
+    NW_HIPCHK(hipSetDevice(t->device));
+    nw_walk_state* w = nullptr;
+    if ((rc = walk_state(t, &w))) return rc;
+    const int64_t N = L2 + 1;
+    const size_t need = (size_t)(L1 + 1) * (size_t)N * 8;
+    if (w->cnt_serial != t->fill_serial) {
+        if (w->cnt_bytes < need) {
+            (void)hipFree(w->cnt);
+            w->cnt = nullptr;
+            w->cnt_bytes = 0;
+            NW_HIPCHK(hipMalloc(&w->cnt, need));
+            w->cnt_bytes = need;
+        }
+        const nwk::TableView v = nwk::view_of(t);
+        nw_count_border_kernel<<<256, 256, 0, t->stream>>>(w->cnt, L1, L2);
+        NW_HIPCHK(hipGetLastError());
+        const int nti = (int)((L1 + CT - 1) / CT), ntj = (int)((L2 + 63) / 64);
+        for (int dg = 0; L1 > 0 && L2 > 0 && dg < nti + ntj - 1; ++dg) {
+            const int lo = std::max(0, dg - (nti - 1)), hi = std::min(dg, ntj - 1);
+            nw_count_tiles_kernel<<<hi - lo + 1, 64, 0, t->stream>>>(v, w->cnt, L1, L2, dg, ntj);
+        }
+        NW_HIPCHK(hipGetLastError());
+        NW_HIPCHK(hipStreamSynchronize(t->stream));
+        w->cnt_serial = t->fill_serial;
+    }
+    uint64_t tot = 0;
+    if (L1 > 0 || L2 > 0)   // two empty strings: the reference's walk prints nothing (see count_alignments)
+        NW_HIPCHK(hipMemcpy(&tot, w->cnt + L1 * N + L2, 8, hipMemcpyDeviceToHost));
+    if (total) *total = tot;
+    const uint64_t avail = first < tot ? tot - first : 0;
+    const uint64_t todo = std::min(count, avail);
+    // batches bounded by 64 MB of moves on the device
+    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, ((uint64_t)64 << 20) / (uint64_t)std::max<int64_t>(stride, 1)));
+    const size_t mb = (size_t)(std::min(per, std::max<uint64_t>(todo, 1)) * (uint64_t)std::max<int64_t>(stride, 1));
+    if (todo && (w->ebytes < mb || w->elens_n < std::min(per, todo))) {
+        (void)hipFree(w->emoves);
+        (void)hipFree(w->elens);
+        w->emoves = nullptr;
+        w->elens = nullptr;
+        w->ebytes = w->elens_n = 0;
+        NW_HIPCHK(hipMalloc(&w->emoves, mb));
+        NW_HIPCHK(hipMalloc(&w->elens, (size_t)std::min(per, todo) * 4));
+        w->ebytes = mb;
+        w->elens_n = (size_t)std::min(per, todo);
+    }
+    const nwk::TableView v = nwk::view_of(t);
+    for (uint64_t done = 0; done < todo;) {
+        const uint64_t b = std::min(per, todo - done);
+        nw_unrank_kernel<<<(unsigned)std::min<uint64_t>((b + 255) / 256, 4096), 256, 0, t->stream>>>(
+            v, w->cnt, L1, L2, first + done, b, tot, w->emoves, stride, w->elens);
+        NW_HIPCHK(hipGetLastError());
+        NW_HIPCHK(hipMemcpyAsync(moves + done * (uint64_t)stride, w->emoves, (size_t)(b * (uint64_t)stride),
+                                 hipMemcpyDeviceToHost, t->stream));
+        NW_HIPCHK(hipMemcpyAsync(lens + done, w->elens, (size_t)b * 4, hipMemcpyDeviceToHost, t->stream));
+        NW_HIPCHK(hipStreamSynchronize(t->stream));
+        done += b;
+    }
+    for (uint64_t p = todo; p < count; ++p) lens[p] = 0;
+    if (n_out) *n_out = todo;
+    return NW_OK;
 }
 
 }  // extern "C"

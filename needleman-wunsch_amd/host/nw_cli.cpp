@@ -3,8 +3,10 @@
 // Same options, operands, messages and exit codes as the reference driver
 // (needleman-wunsch.c:65-89 usage, :698-795 main, dbg.c:7-15 program name,
 // dbg.h:67-100 error format).  Between reading the sequences and printing,
-// compute_table_scores() (needleman-wunsch.c:583) is replaced by nw_fill()
-// (include/nw_fill.h) on the GPU.  -p N is accepted and validated exactly as
+// compute_table_scores() (needleman-wunsch.c:583) is replaced by a
+// device-resident nw_table fill (include/nw_fill.h) on the GPU, and the
+// traceback's enumeration by nw_table_enumerate_paths (one device thread per
+// alignment, in the reference's order).  -p N is accepted and validated exactly as
 // in the reference (it must be > 1) but the fill always runs on the GPU:
 // there is no CPU path.  Failure to run the GPU fill is an error (exit 1).
 #include <getopt.h>
@@ -14,6 +16,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -50,6 +53,41 @@ void log_err_errno(const char* msg) {
           "  -u   use unicode arrows when printing the scores table\n",
           stderr);
     exit(1);
+}
+
+// Alignments in print order, fetched from the device in batches
+// (nw_table_enumerate_paths) for nwh_render_paths.
+struct PathBatches {
+    nw_table* t = nullptr;
+    int64_t stride = 1;
+    uint64_t next = 0;          // first alignment of the next batch
+    uint64_t have = 0, pos = 0; // alignments in the buffers / handed out
+    std::vector<uint8_t> moves;
+    std::vector<int32_t> lens;
+    int rc = NW_OK;
+};
+
+int next_path(void* ctx, const uint8_t** mv, int64_t* n) {
+    auto* b = static_cast<PathBatches*>(ctx);
+    if (b->pos == b->have) {
+        const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(1u << 16, ((uint64_t)256 << 20) / (uint64_t)b->stride));
+        if (b->lens.size() < want) {
+            b->moves.resize((size_t)(want * (uint64_t)b->stride));
+            b->lens.resize((size_t)want);
+        }
+        uint64_t got = 0;
+        b->rc = nw_table_enumerate_paths(b->t, b->next, want, b->moves.data(), b->stride, b->lens.data(), &got,
+                                         nullptr);
+        if (b->rc != NW_OK) return -1;
+        b->have = got;
+        b->pos = 0;
+        b->next += got;
+        if (got == 0) return 0;
+    }
+    *mv = b->moves.data() + b->pos * (uint64_t)b->stride;
+    *n = b->lens[(size_t)b->pos];
+    ++b->pos;
+    return 1;
 }
 
 }  // namespace
@@ -108,55 +146,52 @@ int main(int argc, char** argv) {
     const int d = atoi(argv[optind + 2]);
 
     // ---- the fill (GPU) -----------------------------------------------------
+    // The table stays on the device.  What the reference derives from it on
+    // the host comes from the device too: the alignment count for -s
+    // (nw_table_count_alignments), the alignments themselves, in print order,
+    // for plain / -l output (nw_table_enumerate_paths: each one unranked on
+    // its own, the parallel traceback of README:195-200); only -t copies the
+    // scores and codes to the host for the table printer.
     const int64_t L1 = (int64_t)strlen(s1), L2 = (int64_t)strlen(s2);
-    if (f.qflag && f.sflag && !f.lflag && !f.tflag) {
-        // `-q -s` prints only the summary (needleman-wunsch.c:667-673).  The
-        // reference gets the count by enumerating every alignment; the count
-        // is the number of code paths, computed on the device from the
-        // direction codes left in HBM -- no host tables, any size that fits.
-        nw_table* t = nullptr;
-        nw_stats st{};
-        uint32_t count = 0;
-        int rc = nw_table_create(-1, L1, L2, NW_OUT_DIRS, &t);
-        if (rc == NW_OK) rc = nw_table_set_sequences(t, s1, L1, s2, L2);
-        if (rc == NW_OK) rc = nw_table_fill(t, m, k, d, NW_OUT_DIRS);
-        if (rc == NW_OK) rc = nw_table_stats(t, &st);
-        if (rc == NW_OK) rc = nw_table_count_alignments(t, &count);
-        if (rc != NW_OK) {
-            fprintf(stderr, "%s: error: GPU fill failed: %s: %s\n", g_prog, nw_strerror(rc), nw_last_error());
-            exit(1);
-        }
-        nw_table_destroy(t);
-        nwh_print_summary(count, st.corner, stderr);
-        free(s1);
-        free(s2);
-        if (in != stdin) fclose(in);
-        return 0;
-    }
-    const int64_t ncell = (L1 + 1) * (L2 + 1);
-    const bool want_codes = nwh_needs_traceback(&f) || f.tflag;
-    std::vector<int32_t> H;
-    std::vector<uint8_t> nib, codes;
-    if (f.tflag) H.resize((size_t)ncell);
-    if (want_codes) nib.resize((size_t)((ncell + 1) / 2));
+    const bool listing = nwh_needs_traceback(&f) && (!f.qflag || f.lflag);
+    const uint32_t mask = (listing || f.sflag || f.tflag ? (uint32_t)NW_OUT_DIRS : 0u) |
+                          (f.tflag ? (uint32_t)(NW_OUT_SCORES | NW_OUT_STATS) : 0u);
+    nw_table* t = nullptr;
     nw_stats st{};
-    const int rc = nw_fill(s1, L1, s2, L2, m, k, d, f.tflag ? (uint32_t)NW_OUT_STATS : 0u, -1, f.tflag ? H.data() : nullptr,
-                           want_codes ? nib.data() : nullptr, &st);
+    uint32_t count = 0;
+    std::vector<int32_t> H;
+    std::vector<uint8_t> codes;
+    int rc = nw_table_create(-1, L1, L2, mask, &t);
+    if (rc == NW_OK) rc = nw_table_set_sequences(t, s1, L1, s2, L2);
+    if (rc == NW_OK) rc = nw_table_fill(t, m, k, d, mask);
+    if (rc == NW_OK) rc = nw_table_stats(t, &st);
+    if (rc == NW_OK && f.sflag) rc = nw_table_count_alignments(t, &count);
+    if (rc == NW_OK && f.tflag) {
+        const int64_t ncell = (L1 + 1) * (L2 + 1);
+        H.resize((size_t)ncell);
+        codes.resize((size_t)ncell);
+        rc = nw_table_copy_scores(t, 0, L1 + 1, H.data());
+        if (rc == NW_OK) rc = nw_table_copy_codes(t, 0, L1 + 1, codes.data());
+    }
     if (rc != NW_OK) {
         fprintf(stderr, "%s: error: GPU fill failed: %s: %s\n", g_prog, nw_strerror(rc), nw_last_error());
         exit(1);
     }
-    if (want_codes) {
-        codes.resize((size_t)ncell);
-        for (int64_t x = 0; x < ncell; ++x) codes[(size_t)x] = (uint8_t)((nib[(size_t)(x >> 1)] >> (4 * (x & 1))) & 0xf);
-        std::vector<uint8_t>().swap(nib);
+    PathBatches pb;
+    pb.t = t;
+    pb.stride = std::max<int64_t>(L1 + L2, 1);
+    const int r = nwh_render_paths(s1, s2, &f, f.tflag ? H.data() : nullptr, f.tflag ? codes.data() : nullptr,
+                                   st.corner, st.greatest_abs_interior, count, next_path, &pb, stdout, stderr);
+    if (r == -2) {
+        fprintf(stderr, "%s: error: GPU traceback failed: %s: %s\n", g_prog, nw_strerror(pb.rc), nw_last_error());
+        exit(1);
     }
-    if (nwh_render(s1, s2, &f, f.tflag ? H.data() : nullptr, want_codes ? codes.data() : nullptr, st.corner,
-                   st.greatest_abs_interior, stdout, stderr) != 0) {
+    if (r != 0) {
         errno = ENOMEM;
         log_err_errno("malloc failed");
         exit(1);
     }
+    nw_table_destroy(t);
     free(s1);
     free(s2);
     if (in != stdin) fclose(in);

@@ -46,6 +46,24 @@ int nwh_render(const char *s1, const char *s2, const nwh_flags *f,
                const int32_t *H, const uint8_t *codes, int32_t corner,
                int32_t gav, FILE *out, FILE *err);
 
+/* Source of the alignments for nwh_render_paths: sets *moves / *n to the next
+ * alignment in print order -- its moves from (L1,L2) back to (0,0), 1 = diag,
+ * 2 = up, 4 = left (nw_table_enumerate_paths) -- and returns 1; returns 0
+ * after the last one, < 0 on failure. */
+typedef int (*nwh_next_path)(void *ctx, const uint8_t **moves, int64_t *n);
+
+/* nwh_render with the alignments supplied by `next` (the device enumeration)
+ * instead of the host depth-first walk: prints them as the walk would
+ * (needleman-wunsch.c:245-254), then the summary with `solutions`, then the
+ * table, its optimal-path cells being those reachable from the corner along
+ * the codes -- exactly the cells the reference's complete walk visits.
+ * codes: needed for -t; H: for -t.  Returns 0, -1 on allocation failure, -2
+ * when `next` fails. */
+int nwh_render_paths(const char *s1, const char *s2, const nwh_flags *f,
+                     const int32_t *H, const uint8_t *codes, int32_t corner,
+                     int32_t gav, unsigned solutions, nwh_next_path next,
+                     void *ctx, FILE *out, FILE *err);
+
 /* The summary print_summary() writes under -s (computation.c:271-281):
  * "<n> optimal alignment[s]" and "Optimal score is <corner>". */
 void nwh_print_summary(unsigned solutions, int32_t corner, FILE *err);

@@ -163,6 +163,61 @@ int nwh_render(const char* s1, const char* s2, const nwh_flags* f, const int32_t
     return 0;
 }
 
+int nwh_render_paths(const char* s1, const char* s2, const nwh_flags* f, const int32_t* H, const uint8_t* codes,
+                     int32_t corner, int32_t gav, unsigned solutions, nwh_next_path next, void* ctx, FILE* out,
+                     FILE* err) {
+    nwh::Render r{s1, s2, (int64_t)strlen(s1), (int64_t)strlen(s2), *f, H, codes, out, err};
+    const int64_t M = r.L1 + 1, N = r.L2 + 1;
+    try {
+        if (nwh_needs_traceback(f) && (!f->qflag || f->lflag)) {
+            std::vector<char> X((size_t)(M + N)), Y((size_t)(M + N));
+            for (;;) {
+                const uint8_t* mv = nullptr;
+                int64_t n = 0;
+                const int got = next(ctx, &mv, &n);
+                if (got < 0) return -2;
+                if (got == 0) break;
+                int64_t i = r.L1, j = r.L2;
+                for (int64_t q = 0; q < n; ++q) {   // X / Y back to front, as the walk fills them
+                    if (mv[q] == 1) {
+                        X[(size_t)q] = s1[--i];
+                        Y[(size_t)q] = s2[--j];
+                    } else if (mv[q] == 4) {
+                        X[(size_t)q] = s1[--i];
+                        Y[(size_t)q] = '-';
+                    } else {
+                        X[(size_t)q] = '-';
+                        Y[(size_t)q] = s2[--j];
+                    }
+                }
+                nwh::print_alignment(r, X.data(), Y.data(), n - 1);
+            }
+        }
+        if (f->sflag) nwh_print_summary(solutions, corner, err);
+        if (f->tflag) {   // needleman-wunsch.c:677-685
+            // The complete walk visits every cell reachable from the corner
+            // along the codes (each such cell has a path on to (0,0)); two
+            // empty strings: the walk never runs.
+            std::vector<uint16_t> walk((size_t)(M * N), 0);
+            if (r.L1 > 0 || r.L2 > 0) walk[(size_t)(M * N - 1)] = nwh::WALK_OPT;
+            for (int64_t i = r.L1; i >= 0; --i)
+                for (int64_t j = r.L2; j >= 0; --j) {
+                    const size_t c = (size_t)(i * N + j);
+                    if (!(walk[c] & nwh::WALK_OPT)) continue;
+                    const uint8_t code = (uint8_t)(codes[c] & 7);
+                    if ((code & 1) && i > 0 && j > 0) walk[c - (size_t)N - 1] |= nwh::WALK_OPT;
+                    if ((code & 4) && i > 0) walk[c - (size_t)N] |= nwh::WALK_OPT;
+                    if ((code & 2) && j > 0) walk[c - 1] |= nwh::WALK_OPT;
+                }
+            if (f->qflag != 1 || f->sflag == 1 || f->lflag == 1) fputc('\n', out);
+            nwh::print_table(r, walk, gav);
+        }
+    } catch (const std::bad_alloc&) {
+        return -1;
+    }
+    return 0;
+}
+
 void nwh_print_summary(unsigned solutions, int32_t corner, FILE* err) {   // computation.c:271-281
     fprintf(err, "%d optimal alignment%s\n", (int)solutions, solutions > 1 ? "s" : "");
     fprintf(err, "Optimal score is %-d\n", corner);

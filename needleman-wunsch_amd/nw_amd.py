@@ -58,7 +58,7 @@ EXPORTS = (
     "nw_table_copy_codes", "nw_table_copy_last_column", "nw_table_score_pitch", "nw_table_waves",
     "nw_table_trace", "nw_table_count_alignments", "nw_table_first_path", "nw_table_walk_elapsed_ms",
     "nw_first_path_banded", "nw_table_hash_columns", "nw_hash_fold",
-    "nw_host_alloc", "nw_host_free", "nw_table_io_stats",
+    "nw_host_alloc", "nw_host_free", "nw_table_io_stats", "nw_table_enumerate_paths",
     # include/nw_panel.h
     "nw_panel_partition", "nw_panel_chain", "nw_panel_get_id", "nw_panel_create", "nw_panel_ipc_handle",
     "nw_panel_ipc_connect", "nw_panel_group_create", "nw_panel_destroy", "nw_panel_set_sequences",
@@ -158,6 +158,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "nw_first_path_banded": (c_int, [c_int, ctypes.c_char_p, c_i64, ctypes.c_char_p, c_i64, c_i32, c_i32, c_i32,
                                          c_i64, c_p, c_i64, P(c_i64)]),
         "nw_host_alloc": (c_int, [ctypes.c_size_t, P(c_p)]),
+        "nw_table_enumerate_paths": (c_int, [c_p, ctypes.c_uint64, ctypes.c_uint64, c_p, c_i64, c_p,
+                                             P(ctypes.c_uint64), P(ctypes.c_uint64)]),
         "nw_host_free": (None, [c_p]),
         "nw_table_io_stats": (c_int, [c_p, P(ctypes.c_double), P(c_i64), P(ctypes.c_double), P(c_i64)]),
     }
@@ -334,6 +336,18 @@ class Table:
         out = _out(out, (i1 - i0, self.L2 + 1), np.uint8)
         _check(self._lib.nw_table_copy_codes(self._h, i0, i1, out.ctypes.data), "nw_table_copy_codes")
         return out
+
+    def enumerate_paths(self, first: int = 0, count: int = 1) -> tuple[list[np.ndarray], int]:
+        """Alignments first .. first+count-1 in the reference's print order, each
+        as its moves from the corner back to (0,0) (1 diag, 2 up, 4 left), and the
+        total number of alignments (nw_table_enumerate_paths)."""
+        stride = max(self.L1 + self.L2, 1)
+        mv = np.zeros((max(count, 1), stride), dtype=np.uint8)
+        ln = np.zeros(max(count, 1), dtype=np.int32)
+        n, tot = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self._lib.nw_table_enumerate_paths(self._h, first, count, mv.ctypes.data, stride, ln.ctypes.data,
+                                                  ctypes.byref(n), ctypes.byref(tot)), "nw_table_enumerate_paths")
+        return [mv[p, :ln[p]].copy() for p in range(n.value)], tot.value
 
     def io_stats(self) -> dict:
         """Last upload / slice copy: wall ms and bytes (nw_table_io_stats)."""
