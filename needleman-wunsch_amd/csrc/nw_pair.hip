@@ -459,7 +459,7 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                     __builtin_amdgcn_s_sleep(1);
                 }
             };
-            auto full_chunk = [&](int c, auto slotc, const PairSlot& cur, PairSlot& nxt) -> bool {
+            auto full_chunk = [&](int c, auto slotc, PairSlot& cur, PairSlot& nxt) -> bool {
                 constexpr int Q = decltype(slotc)::value;
                 pair_chunk_asm<SH || ST, SD || ST, ST, PROF>(r, kc, cur, nxt, c + 1, ra[Q], rd[(Q + 1) % R]);
                 if (SH) {

@@ -38,6 +38,12 @@ ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 OUT = os.path.join(ROOT, "needleman-wunsch_amd", "csrc", "nw_pair_chunk.inc")
 READ_AT = 6            # step whose gaps issue the next slot's progress and data reads
 ALIGN = None           # None, or the byte phase (0 / 4) mod 8 at which every block starts
+# The DPP shift of column s writes into the register of T_{s-1} (the row
+# above at column s-1, not needed after column s-1's max3): lanes >= 1 take
+# the shifted Gb, lane 0 keeps T_{s-1} -- the value the shift must give it --
+# so no per-column v_mov pre-fill of lane 0 (only the block's last, into the
+# carried shc).  The T operands become read-write.
+SHIFT_INTO_T = True
 
 
 def GA(s):
@@ -49,6 +55,8 @@ def GB(s):
 
 
 def SH(s):
+    if SHIFT_INTO_T and 1 <= s <= 7:
+        return T(s - 1)      # the shift overwrites T_{s-1}, whose lane 0 it keeps
     return "shc" if s in (0, 8) else f"sh{s}"
 
 
@@ -172,7 +180,8 @@ def block(ST, P, HH=True, FF=True):
         pool = []
         if s > 0:
             pool += column_items(s - 1, ST, HH, FF)
-        pool.append(It("P", f"v_mov_b32_e32 %[{SH(s + 1)}], %[{T(s)}]"))            # lane 0's next shift
+        if not SHIFT_INTO_T or s == 7:
+            pool.append(It("P", f"v_mov_b32_e32 %[{SH(s + 1)}], %[{T(s)}]"))        # lane 0's next shift
         pool += mem.get(s, [])
         chain = []
         if s > 0:
@@ -266,10 +275,10 @@ OPERANDS = r'''
       [hb0] "=&v"(r.hb[0]), [hb1] "=&v"(r.hb[1]), [hb2] "=&v"(r.hb[2]), [hb3] "=&v"(r.hb[3]),              \
       [hb4] "=&v"(r.hb[4]), [hb5] "=&v"(r.hb[5]), [hb6] "=&v"(r.hb[6]), [hb7] "=&v"(r.hb[7]),              \
       [accA] "=&v"(r.accA), [accB] "=&v"(r.accB), [gavA] "+v"(r.gavA), [gavB] "+v"(r.gavB),                 \
-      [pq] "=&v"(r.pq), [nA] "=&v"(ns.a), [nB] "=&v"(ns.b), [nC] "=&v"(ns.c)                               \
-    : [ta0] "v"(ts.a[0]), [ta1] "v"(ts.a[1]), [ta2] "v"(ts.a[2]), [ta3] "v"(ts.a[3]),                      \
-      [tb0] "v"(ts.b[0]), [tb1] "v"(ts.b[1]), [tb2] "v"(ts.b[2]), [tb3] "v"(ts.b[3]),                      \
-      [tc0] "v"(ts.c[0]), [tc1] "v"(ts.c[1]),                                                              \
+      [pq] "=&v"(r.pq), [nA] "=&v"(ns.a), [nB] "=&v"(ns.b), [nC] "=&v"(ns.c),                              \
+      [ta0] "+v"(ts.a[0]), [ta1] "+v"(ts.a[1]), [ta2] "+v"(ts.a[2]), [ta3] "+v"(ts.a[3]),                  \
+      [tb0] "+v"(ts.b[0]), [tb1] "+v"(ts.b[1]), [tb2] "+v"(ts.b[2]), [tb3] "+v"(ts.b[3])                   \
+    : [tc0] "v"(ts.c[0]), [tc1] "v"(ts.c[1]),                                                              \
       [kd0] "v"(k.kd[0]), [kd1] "v"(k.kd[1]), [kd2] "v"(k.kd[2]), [kd3] "v"(k.kd[3]),                      \
       [kd4] "v"(k.kd[4]), [kd5] "v"(k.kd[5]), [kd6] "v"(k.kd[6]), [kd7] "v"(k.kd[7]),                      \
       [nloa] "v"(r.nloa), [nlob] "v"(r.nlob), [c2a] "v"(k.c2a), [c2b] "v"(k.c2b), [vcm] "v"(k.vcm),         \
@@ -293,7 +302,7 @@ def main():
     parts = ["// GENERATED by tools/gen_pair_asm.py -- do not edit; see the generator for the schedule.\n",
              OPERANDS,
              "template <bool HH, bool FF, bool ST, bool P>\n"
-             "__device__ __forceinline__ void pair_chunk_asm(PairRegs& r, const PairConst& k, const PairSlot& ts,\n"
+             "__device__ __forceinline__ void pair_chunk_asm(PairRegs& r, const PairConst& k, PairSlot& ts,\n"
              "                                               PairSlot& ns, int cv, int ra, int rd);\n"]
     decl = "    int ga_[7], gb_[7], sh_[8], xa_[2], dga_[2], dgb_[2], t_[8], sp_[4];\n"
     tf = lambda b: "true" if b else "false"
@@ -304,7 +313,7 @@ def main():
             parts.append(f"// VALU pair_chunk_asm<{tf(HH)}, {tf(FF)}, {tf(ST)}, {tf(P)}>: {nvalu} per 8 columns x 128 rows\n")
             parts.append(
                 f"template <> __device__ __forceinline__ void pair_chunk_asm<{tf(HH)}, {tf(FF)}, {tf(ST)}, {tf(P)}>"
-                f"(PairRegs& r, const PairConst& k, const PairSlot& ts, PairSlot& ns, int cv, int ra, int rd) {{\n"
+                f"(PairRegs& r, const PairConst& k, PairSlot& ts, PairSlot& ns, int cv, int ra, int rd) {{\n"
                 f"{decl}    asm volatile(\n{cstr(lines)}\n"
                 f"        NW_PAIR_OPERANDS : \"vcc\", \"memory\");\n}}\n")
     parts.append("#undef NW_PAIR_OPERANDS\n")
