@@ -116,7 +116,7 @@ __device__ __forceinline__ int g_of(const ChunkRegs& r, int s) {
 // The last chunk of a stripe (n = 1..8 columns): block + flush.  Returns H
 // of the stripe's last column (for the score-only last column).
 template <bool SH, bool SD, bool ST, bool P, int N>
-__device__ __forceinline__ int run_last(ChunkRegs& r, const ChunkConst& k, const RingSlot& t, int ra) {
+__device__ __forceinline__ int run_last(ChunkRegs& r, const ChunkConst& k, RingSlot& t, int ra) {
     RingSlot n;
     chunk_asm<SH, SD, ST, P, N, false>(r, k, t, n, ra, 0);
     flush_asm<SH, SD, ST, N>(r, k, t, ra);
@@ -124,7 +124,7 @@ __device__ __forceinline__ int run_last(ChunkRegs& r, const ChunkConst& k, const
     else return g_of(r, N - 1) + r.nlo + k.kd[N - 1];
 }
 template <bool SH, bool SD, bool ST, bool P>
-__device__ __forceinline__ int run_last_n(int n, ChunkRegs& r, const ChunkConst& k, const RingSlot& t, int ra) {
+__device__ __forceinline__ int run_last_n(int n, ChunkRegs& r, const ChunkConst& k, RingSlot& t, int ra) {
     switch (n) {
         case 1: return run_last<SH, SD, ST, P, 1>(r, k, t, ra);
         case 2: return run_last<SH, SD, ST, P, 2>(r, k, t, ra);
@@ -501,7 +501,7 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
             // One full (non-final) chunk; SLOTC = c % R is a compile-time ring
             // slot.  The block reads the next slot into nxt; the slow path
             // re-reads it when the progress values it saw were too early.
-            auto full_chunk = [&](int c, auto slotc, const RingSlot& cur, RingSlot& nxt) -> bool {
+            auto full_chunk = [&](int c, auto slotc, RingSlot& cur, RingSlot& nxt) -> bool {
                 constexpr int Q = decltype(slotc)::value;
                 constexpr int NQ = (Q + 1) % R;
 #if NW_SCORE_X4
@@ -877,10 +877,10 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         // wavefront (nw_skew.hip); they write different tile layouts
         // (TableView.skew).  The skew kernel's critical path is L1 + 72*NG
         // steps of ~110 cycles, the scan's L1 steps of ~150-230 cycles plus
-        // ~1.2 us per stripe, so the skew kernel wins only on wide tables with
-        // few stripes (measured: 1M x 20k 61 vs 75 ms, 100k x 64 4.6 vs
-        // 6.2 ms; 100k x 100k 22 vs 11 ms).  $NW_KERNEL = scan |
-        // skew | auto (default).
+        // ~1.2 us per stripe, so the skew kernel wins only on very wide tables
+        // with few stripes (measured: 1M x 20k 61 vs 75 ms, 100k x 64 4.6 vs
+        // 6.2 ms; 100k x 12.5k 8.0 vs 7.0 ms and 100k x 100k 22 vs 11 ms the
+        // other way).  $NW_KERNEL = scan | skew | pair | auto (default).
         const char* ke = getenv("NW_KERNEL");
         if (ke && std::strcmp(ke, "skew") == 0) skew = true;
         else if (ke && std::strcmp(ke, "scan") == 0) skew = false;
@@ -892,9 +892,12 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
             // scan kernel then doubles up waves and runs at the two-wave
             // rate); the skew kernel for wide tables with few stripes; the
             // scan kernel otherwise.
+            // (skew from L1 >= 32*L2: it won at 100k x 64 and 1M x 20k, lost
+            // at 100k x 12.5k -- an 8-GPU row panel -- 8.03 vs 7.04 ms,
+            // profiles/r02_ab_loader.txt)
             const int64_t simds = 4 * (int64_t)t->ncu;
             pair = t->NG > simds;
-            skew = !pair && t->NG <= simds && L1 >= 4 * L2;
+            skew = !pair && t->NG <= simds && L1 >= 32 * L2;
         }
         // a feeding panel's last row must be lane 63's row b of its last pair stripe
         if (pair && t->xout && L2 % 128 != 0) pair = false;

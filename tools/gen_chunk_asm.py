@@ -67,13 +67,22 @@ def gname(s):
     return {-2: "gp6", -1: "gin", 6: "gp6", 7: "gin"}.get(s, f"g{s}")
 
 
+SHIFT_INTO_T = True    # the DPP of step s writes into T'_{s-1}'s register (see shreg)
+
+
 def shreg(s):
     """Register of sh_s = wave_shr1(G'_{s-1}) with T'_{s-1} in lane 0: the DPP
-    leaves lane 0 (no source lane) at the register's old value, so it is
-    pre-filled with T'_{s-1} (tm: the previous chunk's T'_7; the others by a
-    v_mov scheduled into a free gap slot).  Three rotate, so the pre-fill of
-    step s can go anywhere in steps s-2 .. s-1."""
-    return "tm" if s == 0 else f"sh{s % 3}"
+    leaves lane 0 (no source lane) at the register's old value.  Steps 1..7
+    shift into T'_{s-1}'s own register (read for the last time by X_{s-1}'s
+    max3), so lane 0 already holds T'_{s-1} and no pre-fill is needed (the T'
+    operands are read-write); step 0 uses tm (the previous chunk's T'_7), and
+    the flush of a full chunk's last column a rotating sh register with a
+    pre-fill."""
+    if s == 0:
+        return "tm"
+    if SHIFT_INTO_T and s <= 7:
+        return f"t{s - 1}"
+    return f"sh{s % 3}"
 
 
 def dg_reg(s):
@@ -161,7 +170,7 @@ def floating_items(N, nxt, P=False):
     """
     last = N - 1
     its = [Item(f"SH{s}", f"v_mov_b32_e32 %[{shreg(s)}], %[t{s - 1}]", lo=max(s - 2, 0), hi=s - 1)
-           for s in range(1, N)]
+           for s in range(1, N) if shreg(s) != f"t{s - 1}"]
     if P and N > 4:                  # profile lookup of steps 4..7, before step 4
         its.append(Item("PB", "v_perm_b32 %[subB], %[ph], %[pl], %[t9]", hi=3))
     its += [Item("CW", "ds_write_b32 %[cb], %[cv] offset:4", lds=True, hi=last),  # ring slot taken
@@ -304,7 +313,7 @@ def flush(N, F, H, A, S):
     if F:
         sh = shreg(s)
         items = {it.name: it.text for it in code_items(s, sh, False)}
-        out += [f"v_mov_b32_e32 %[{sh}], %[t{s - 1}]", items["L"], items["D"],
+        out += ([] if sh == f"t{s - 1}" else [f"v_mov_b32_e32 %[{sh}], %[t{s - 1}]"]) + [items["L"], items["D"],
                 f"v_mov_b32_dpp %[{sh}], %[{gname(s - 1)}] wave_shr:1 row_mask:0xf bank_mask:0xf",
                 items["U"], items["b1"], items["b2"], items["b3"],
                 f"v_xor_b32_e32 %[accp], {hex((1 << 3 * N) - 1)}, %[accp]"]     # (flags were collected inverted)
@@ -326,9 +335,10 @@ OPERANDS = r'''
       [accp] "+v"(r.accp), [acc] "=&v"(r.acc), [gav] "+v"(r.gav), [tmp] "=&v"(tmp_),                      \
       [dL] "=&v"(dL_), [dU] "=&v"(dU_), [dD] "=&v"(dD_),                                \
       [cv] "+v"(r.cv), [hv] "+v"(r.hv), [dv] "+v"(r.dv),         \
-      [nlo] "+v"(r.nlo)                                                                                    \
-    : [t0] "v"(ts.a[0]), [t1] "v"(ts.a[1]), [t2] "v"(ts.a[2]), [t3] "v"(ts.a[3]),                          \
-      [t4] "v"(ts.b[0]), [t5] "v"(ts.b[1]), [t6] "v"(ts.b[2]), [t7] "v"(ts.b[3]), [t8] "v"(ts.c[0]),         \
+      [nlo] "+v"(r.nlo),                                                                                   \
+      [t0] "+v"(ts.a[0]), [t1] "+v"(ts.a[1]), [t2] "+v"(ts.a[2]), [t3] "+v"(ts.a[3]),                      \
+      [t4] "+v"(ts.b[0]), [t5] "+v"(ts.b[1]), [t6] "+v"(ts.b[2]), [t7] "+v"(ts.b[3])                       \
+    : [t8] "v"(ts.c[0]),                                                                                   \
       [t9] "v"(ts.c[1]), [c2] "v"(k.c2), [vcm] "v"(k.vcm), [vck] "v"(k.vck), [d8] "s"(k.d8),                                \
       [k0] "v"(k.kd[0]), [k1] "v"(k.kd[1]), [k2] "v"(k.kd[2]), [k3] "v"(k.kd[3]),                          \
       [k4] "v"(k.kd[4]), [k5] "v"(k.kd[5]), [k6] "v"(k.kd[6]), [k7] "v"(k.kd[7]),                          \
@@ -366,10 +376,10 @@ def main():
              f"#define NW_SCORE_X4 {int(SCORE_X4)}\n#define NW_SCORE_HINT \"{(' ' + STORE_HINT) if STORE_HINT else ''}\"\n",
              OPERANDS, FLUSH_OPERANDS,
              "template <bool SH, bool SD, bool ST, bool P, int N, bool NEXT>\n"
-             "__device__ __forceinline__ void chunk_asm(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts,\n"
+             "__device__ __forceinline__ void chunk_asm(ChunkRegs& r, const ChunkConst& k, RingSlot& ts,\n"
              "                                          RingSlot& ns, int ra, int rd);\n"
              "template <bool SH, bool SD, bool ST, int N>\n"
-             "__device__ __forceinline__ void flush_asm(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts, int ra);\n"]
+             "__device__ __forceinline__ void flush_asm(ChunkRegs& r, const ChunkConst& k, RingSlot& ts, int ra);\n"]
     decl = "    int tmp_, dL_, dU_, dD_, sh0_, sh1_, sh2_;\n"
     unpack = ""
     for SH in (0, 1):
@@ -382,12 +392,12 @@ def main():
                         for P in (0, 1):
                             parts.append(
                                 f"template <> __device__ __forceinline__ void chunk_asm<{head}, {tf(P)}, {N}, {tf(nxt)}>"
-                                f"(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts, RingSlot& ns, int ra, int rd) {{\n"
+                                f"(ChunkRegs& r, const ChunkConst& k, RingSlot& ts, RingSlot& ns, int ra, int rd) {{\n"
                                 f"{decl}{unpack}    asm volatile(\n{cstr(block(N, F, H, A, S, SD, nxt, P))}\n"
                                 f"        NW_CHUNK_OPERANDS : \"vcc\", \"scc\", \"memory\");\n}}\n")
                     parts.append(
                         f"template <> __device__ __forceinline__ void flush_asm<{head}, {N}>"
-                        f"(ChunkRegs& r, const ChunkConst& k, const RingSlot& ts, int ra) {{\n{decl}"
+                        f"(ChunkRegs& r, const ChunkConst& k, RingSlot& ts, int ra) {{\n{decl}"
                         f"    RingSlot ns;\n    const int rd = 0;\n"
                         f"    asm volatile(\n{cstr(flush(N, F, H, A, S))}\n"
                         f"        NW_FLUSH_OPERANDS : \"vcc\", \"scc\", \"memory\");\n}}\n")
