@@ -89,7 +89,11 @@ constexpr int SLOT = 16;
 // from the producer wave starting a chunk to its granules stored, ~2.5 us
 // more until the next WG-stripe's loader sees them, wherever the two
 // WG-stripes sit (tools/trace_lag.py; an L2-resident second copy for
-// same-XCD consumers and 128-byte padded lines were both slower).
+// same-XCD consumers and 128-byte padded lines were both slower; plain
+// stores with one agent release per batch, 0.43 -> 1.2 us in isolation
+// beside a store stream against 1.9 us for sc1 (tools/ubench_handoff.hip),
+// made the 100k^2 fill 8x slower: the release writes back the L2 that the
+// table stream keeps dirty).
 __device__ __forceinline__ void put_granule(uint64_t* gout, int64_t idx, uint64_t gr) {
     __hip_atomic_store(gout + idx, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
