@@ -690,9 +690,10 @@ struct StripePlan {
 };
 
 // wmax: the most compute waves the kernel takes (the pair kernel adds a
-// publisher wave to the loader, so it stops at 12).
-StripePlan plan_stripes(int64_t NG, int ncu, int wmax = 15) {
-    StripePlan p{8, (NG + 7) / 8, 8, 0};
+// publisher wave to the loader, so it stops at 12); wfix: the WG-stripe
+// height of the dequeued plan.
+StripePlan plan_stripes(int64_t NG, int ncu, int wmax = 15, int wfix = 8) {
+    StripePlan p{wfix, (NG + wfix - 1) / wfix, wfix, 0};
     if (const char* e = getenv("NW_WAVES")) {
         const int w = atoi(e);
         for (int c : kWaveChoices)
@@ -903,7 +904,12 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         if (pair && t->xout && L2 % 128 != 0) pair = false;
         const int64_t NGk = pair ? (L2 + 127) / 128 : t->NG;
         if (pair) {
-            plan = plan_stripes(NGk, t->ncu, 12);
+            // Dequeued WG-stripes (more than 15 pair stripes per CU): 12 high
+            // for score-only fills, whose block fits 128 VGPRs, so three
+            // compute waves share a SIMD (1M^2: 268 vs 292 ms at 8 high,
+            // profiles/r02_ab_loader.txt); 8 when the block also makes
+            // scores / codes (it would spill at 12).
+            plan = plan_stripes(NGk, t->ncu, 12, (sh || sd || stt) ? 8 : 12);
             W = plan.W;
         }
         KernelFn fn = skew ? pick_skew(W, prof, sh, sd, stt)

@@ -33,6 +33,7 @@ compares.
 """
 import argparse
 import os
+import re
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 OUT = os.path.join(ROOT, "needleman-wunsch_amd", "csrc", "nw_pair_chunk.inc")
@@ -44,6 +45,10 @@ ALIGN = None           # None, or the byte phase (0 / 4) mod 8 at which every bl
 # so no per-column v_mov pre-fill of lane 0 (only the block's last, into the
 # carried shc).  The T operands become read-write.
 SHIFT_INTO_T = True
+# Ring writes of lane 63's Gb in pairs of columns (ds_write2_b32 after the odd
+# column) and the two symbol words in one ds_write2_b32: 11 LDS ops a block
+# instead of 16.
+RING2 = True
 
 
 def GA(s):
@@ -97,9 +102,18 @@ def sub_items(s, P, row):
             f"v_add_u32_e32 %[{dst}], %[{src}], %[sub]"]
 
 
+def ring_items(c):
+    """Ring write of lane 63's Gb at column c (the row above of the wave below)."""
+    if not RING2:
+        return [It("R", f"ds_write_b32 %[ra], %[{GB(c)}] offset:{4 * c}", lds=True)]
+    if c % 2 == 0:
+        return []
+    return [It("R", f"ds_write2_b32 %[ra], %[{GB(c - 1)}], %[{GB(c)}] offset0:{c - 1} offset1:{c}", lds=True)]
+
+
 def column_items(c, ST, HH=True, FF=True):
     """Codes (FF), scores (HH), ring write of column c (needs Ga_c final: dep 'F')."""
-    its = [It("R", f"ds_write_b32 %[ra], %[{GB(c)}] offset:{4 * c}", lds=True)]
+    its = ring_items(c)
     if not HH and not FF:
         return its
     if not FF:
@@ -109,7 +123,7 @@ def column_items(c, ST, HH=True, FF=True):
     # row b parts need no F
     its.append(It("Lb", f"v_sub_u32_e32 %[dLb], %[{GB(c - 1)}], %[{GB(c)}]"))
     its.append(It("Hb", f"v_add3_u32 %[hb{c}], %[{GB(c)}], %[nlob], %[kd{c}]"))
-    its.append(It("R", f"ds_write_b32 %[ra], %[{GB(c)}] offset:{4 * c}", lds=True))
+    its += ring_items(c)
     its.append(It("Db", f"v_sub_u32_e32 %[dDb], %[{DGB(c)}], %[{GB(c)}]"))
     its.append(It("Ub", f"v_sub_u32_e32 %[dUb], %[{GA(c)}], %[{GB(c)}]", ["F"]))
     its.append(It("La", f"v_sub_u32_e32 %[dLa], %[{GA(c - 1)}], %[{GA(c)}]", ["F"]))
@@ -159,9 +173,10 @@ def block(ST, P, HH=True, FF=True):
         elif not got:
             out.append(It("", "s_nop 1"))
 
-    mem = {0: [It("CW", "ds_write_b32 %[cb], %[cv] offset:4", lds=True),            # cons[w] = c+1
-               It("W8", "ds_write_b32 %[ra], %[tc0] offset:32", lds=True),          # symbols down the ring
-               It("W9", "ds_write_b32 %[ra], %[tc1] offset:36", lds=True)],
+    sym = ([It("W8", "ds_write2_b32 %[ra], %[tc0], %[tc1] offset0:8 offset1:9", lds=True)] if RING2 else
+           [It("W8", "ds_write_b32 %[ra], %[tc0] offset:32", lds=True),             # symbols down the ring
+            It("W9", "ds_write_b32 %[ra], %[tc1] offset:36", lds=True)])
+    mem = {0: [It("CW", "ds_write_b32 %[cb], %[cv] offset:4", lds=True)] + sym,      # cons[w] = c+1
            # (READ_AT: how late in the block the next slot is read; the
            # producer runs one chunk ahead, so an early read usually misses it
            # and the caller takes the slow re-read)
@@ -287,6 +302,18 @@ OPERANDS = r'''
 '''
 
 
+def operands(text):
+    """The operand lists of one block: only the NW_PAIR_OPERANDS entries its
+    text names (an unbound early-clobber output would still take a VGPR --
+    about 30 in the score-only block)."""
+    outs_txt, ins_txt = OPERANDS.split("    : [tc0]")
+    ins_txt = "[tc0]" + ins_txt
+    pat = re.compile(r'\[(\w+)\] "([^"]*)"\(([^()]*)\)')
+    used = set(re.findall(r"%\[(\w+)\]", text))
+    fmt = lambda lst: ", ".join(f'[{n}] "{c}"({e})' for n, c, e in lst if n in used)
+    return f"        : {fmt(pat.findall(outs_txt))}\n        : {fmt(pat.findall(ins_txt))}\n"
+
+
 def cstr(lines):
     return "\n".join(f'        "{ln}\\n\\t"' for ln in lines)
 
@@ -300,11 +327,10 @@ def main():
     globals()["READ_AT"] = args.read_at
     globals()["ALIGN"] = args.align
     parts = ["// GENERATED by tools/gen_pair_asm.py -- do not edit; see the generator for the schedule.\n",
-             OPERANDS,
              "template <bool HH, bool FF, bool ST, bool P>\n"
              "__device__ __forceinline__ void pair_chunk_asm(PairRegs& r, const PairConst& k, PairSlot& ts,\n"
              "                                               PairSlot& ns, int cv, int ra, int rd);\n"]
-    decl = "    int ga_[7], gb_[7], sh_[8], xa_[2], dga_[2], dgb_[2], t_[8], sp_[4];\n"
+    decl = "    [[maybe_unused]] int ga_[7], gb_[7], sh_[8], xa_[2], dga_[2], dgb_[2], t_[8], sp_[4];\n"
     tf = lambda b: "true" if b else "false"
     for HH, FF, ST in ((1, 1, 1), (1, 1, 0), (1, 0, 0), (0, 1, 0), (0, 0, 0)):
         for P in (0, 1):
@@ -314,9 +340,8 @@ def main():
             parts.append(
                 f"template <> __device__ __forceinline__ void pair_chunk_asm<{tf(HH)}, {tf(FF)}, {tf(ST)}, {tf(P)}>"
                 f"(PairRegs& r, const PairConst& k, PairSlot& ts, PairSlot& ns, int cv, int ra, int rd) {{\n"
-                f"{decl}    asm volatile(\n{cstr(lines)}\n"
-                f"        NW_PAIR_OPERANDS : \"vcc\", \"memory\");\n}}\n")
-    parts.append("#undef NW_PAIR_OPERANDS\n")
+                f"{decl}    asm volatile(\n{cstr(lines)}\n{operands(chr(10).join(lines))}"
+                f"        : \"vcc\", \"memory\");\n}}\n")
     with open(args.out, "w") as f:
         f.write("\n".join(parts))
     print("wrote", args.out)
