@@ -679,10 +679,16 @@ constexpr int kMaxWgPerCu = 4;
 // Compute waves per workgroup (+1 loader wave; 16 waves = 1024 threads max).
 const int kWaveChoices[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 15};
 
-// How the NG 64-row stripes become workgroup stripes.  One WG-stripe per CU
-// when that takes at most 15 waves, the stripes dealt as evenly as possible
-// (SQ or SQ+1 each), so every CU works and each SIMD holds <= 4 stripes;
-// otherwise fixed 8-stripe WG-stripes taken in turn from the dequeue.
+// How the NG stripes become workgroup stripes.  pack4 (scan and pair
+// kernels): while every SIMD can have its own compute wave (NG <= 4 per CU),
+// WG-stripes of 4 stripes (3 or 4, dealt evenly), even if CUs stay idle:
+// a hop inside a workgroup costs ~0.7 us against 3-5 us through granules, and
+// a fifth wave would double up a SIMD (profiles/r02_ab_loader.txt: 10k^2
+// 1.10 -> 0.90 ms, 100k x 12.5k 7.06 -> 6.57 ms, 100k x 25k 7.20 -> 6.98 ms,
+// 100k^2 pair 9.54 -> 9.45 ms).  Otherwise one WG-stripe per CU when that
+// takes at most wmax waves, the stripes dealt as evenly as possible (SQ or
+// SQ+1 each); beyond that fixed wfix-stripe WG-stripes taken in turn from the
+// dequeue.
 struct StripePlan {
     int W;              // kernel's compute waves per workgroup
     int64_t NSW;        // WG-stripes
@@ -692,12 +698,17 @@ struct StripePlan {
 // wmax: the most compute waves the kernel takes (the pair kernel adds a
 // publisher wave to the loader, so it stops at 12); wfix: the WG-stripe
 // height of the dequeued plan.
-StripePlan plan_stripes(int64_t NG, int ncu, int wmax = 15, int wfix = 8) {
+StripePlan plan_stripes(int64_t NG, int ncu, int wmax = 15, int wfix = 8, bool pack4 = false) {
     StripePlan p{wfix, (NG + wfix - 1) / wfix, wfix, 0};
     if (const char* e = getenv("NW_WAVES")) {
         const int w = atoi(e);
         for (int c : kWaveChoices)
             if (c == w && c <= wmax) return StripePlan{w, (NG + w - 1) / w, w, 0};
+    }
+    if (pack4 && NG <= 4 * (int64_t)ncu) {
+        const int W = (int)std::min<int64_t>(4, NG);
+        const int64_t NSW = (NG + W - 1) / W;
+        return StripePlan{W, NSW, (int)(NG / NSW), (int)(NG % NSW)};
     }
     if (NG <= ncu) return StripePlan{1, NG, 1, 0};
     const int SQ = (int)(NG / ncu), SR = (int)(NG % ncu);
@@ -902,6 +913,10 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         }
         // a feeding panel's last row must be lane 63's row b of its last pair stripe
         if (pair && t->xout && L2 % 128 != 0) pair = false;
+        if (!skew && !pair) {
+            plan = plan_stripes(t->NG, t->ncu, 12, 8, true);
+            W = plan.W;
+        }
         const int64_t NGk = pair ? (L2 + 127) / 128 : t->NG;
         if (pair) {
             // Dequeued WG-stripes (more than 15 pair stripes per CU): 12 high
@@ -909,7 +924,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
             // compute waves share a SIMD (1M^2: 268 vs 292 ms at 8 high,
             // profiles/r02_ab_loader.txt); 8 when the block also makes
             // scores / codes (it would spill at 12).
-            plan = plan_stripes(NGk, t->ncu, 12, (sh || sd || stt) ? 8 : 12);
+            plan = plan_stripes(NGk, t->ncu, 12, (sh || sd || stt) ? 8 : 12, true);
             W = plan.W;
         }
         KernelFn fn = skew ? pick_skew(W, prof, sh, sd, stt)
