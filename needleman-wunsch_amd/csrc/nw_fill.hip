@@ -834,6 +834,9 @@ TableView view_of(const nw_table* t) {
     v.NC = (int32_t)t->lay_NC;
     v.skew = t->skew;
     v.pair = t->pair;
+    v.raw = t->raw;
+    v.SQ = t->SQ;
+    v.SR = t->SR;
     v.d = t->last_d;
     v.row_base = (int32_t)t->row_base;
     v.top = t->row_base > 0 ? t->row0 : nullptr;
@@ -876,6 +879,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
     NW_HIPCHK(hipMemsetAsync(t->ctl, 0, CTL_WORDS * 4, t->stream));
     int W = 0;
     bool skew = false, pair = false;
+    int32_t pSQ = 0, pSR = 0;
     if (L1 > 0 && L2 > 0) {
         StripePlan plan = plan_stripes(t->NG, t->ncu, 12);
         W = plan.W;
@@ -944,8 +948,8 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         a.NCH = (int32_t)NCH;
         a.NG = (int32_t)NGk;
         a.NSW = (int32_t)plan.NSW;
-        a.SQ = plan.SQ;
-        a.SR = plan.SR;
+        a.SQ = pSQ = plan.SQ;
+        a.SR = pSR = plan.SR;
         a.H = t->H;
         a.spitch = pair ? 2 * t->spitch : t->spitch;
         a.D = t->D;
@@ -1028,6 +1032,10 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
     t->pend_W = W;
     t->pend_skew = skew;
     t->pend_pair = pair;
+    // the pair kernel's fills with scores and without stats store G' (RAW in nw_pair.hip)
+    t->pend_raw = pair && sh && !stt;
+    t->pend_SQ = pSQ;
+    t->pend_SR = pSR;
     return NW_OK;
 }
 
@@ -1055,6 +1063,8 @@ int fill_finish(nw_table* t) {
         NW_HIPCHK(hipMemcpyAsync(&corner, src, 4, hipMemcpyDeviceToHost, t->stream));
     }
     NW_HIPCHK(hipStreamSynchronize(t->stream));
+    if (L1 > 0 && L2 > 0 && sh && t->pend_raw)
+        corner = (int32_t)((uint32_t)corner - raw_offset(L1, L2, t->pend_SQ, t->pend_SR, d));
     if (ctl[CTL_ERR])
         return fail((int)ctl[CTL_ERR], (int)ctl[CTL_ERR] == NW_ERR_PEER
                                            ? "nw_table_fill: the panel above failed"
@@ -1072,6 +1082,9 @@ int fill_finish(nw_table* t) {
     t->waves = t->pend_W;
     t->skew = t->pend_skew;
     t->pair = t->pend_pair;
+    t->raw = t->pend_raw;
+    t->SQ = t->pend_SQ;
+    t->SR = t->pend_SR;
     t->lay_NC = t->spitch / 512;
     return NW_OK;
 }

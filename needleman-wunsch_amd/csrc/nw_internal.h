@@ -22,6 +22,8 @@ struct nw_table {
     int64_t NC = 0, NG = 0, spitch = 0;   // NC = ceil(L1/8) column chunks; spitch: see fill_launch
     int skew = 0;                   // layout of the tables: 1 = skewed (nw_skew.hip), 0 = column (scan)
     int pair = 0;                   // 1: column layout with rows permuted (nw_pair.hip, nwi::pair_row)
+    int raw = 0;                    // 1: pair tiles hold G' (nwk::raw_offset) under plan SQ / SR
+    int32_t SQ = 0, SR = 0;
     int64_t lay_NC = 0;             // chunks per stripe of that layout
     int alpha = 0;                  // s1/s2 coded to symbols 0..alpha-1 on the device (<= 8), 0: raw bytes
     // device buffers
@@ -57,6 +59,8 @@ struct nw_table {
     int pend_W = 0;
     int pend_skew = 0;
     int pend_pair = 0;
+    int pend_raw = 0;
+    int32_t pend_SQ = 0, pend_SR = 0;
     // results of the last fill
     bool filled = false;
     uint64_t fill_serial = 0;       // completed fills (walk services cache per fill)

@@ -184,6 +184,8 @@ struct TableView {
     int32_t NC;             // chunks per stripe of the layout (scan: ceil(L1/8); skew: ceil((L1+63)/8))
     int32_t skew;           // 1: skewed layout (nw_skew.hip), 0: column layout (scan kernel)
     int32_t pair;           // 1: column layout with rows permuted (nw_pair.hip)
+    int32_t raw;            // 1: the tiles hold the pair kernel's G' (see raw_offset)
+    int32_t SQ, SR;         // raw: the fill's WG-stripe plan (FillArgs)
     int32_t d;
     int32_t row_base;       // panels: global row of local row 0
     const int32_t* top;     // panels: the row above (H - d, nw_table.row0), or null for row 0 = seed
@@ -222,10 +224,26 @@ __host__ __device__ __forceinline__ int64_t code_word(int64_t i, int64_t j, int6
     return (g * (NC + 1) + (t >> 3) + 1) * 64 + l;
 }
 
+// Raw pair tiles (nw_pair.hip, RAW) hold G' = H + r*d + (i - base)*d of the
+// kernel's domain: r = the row's offset inside its WG-stripe (pair stripes
+// g0 = s*SQ + min(s, SR) .. of WG-stripe s, 128 rows each), base = the first
+// column of the cell's 4096-column super-chunk.  H = G' - raw_offset (mod 2^32,
+// as the kernel computes).
+__host__ __device__ __forceinline__ uint32_t raw_offset(int64_t i, int64_t j, int SQ, int SR, int32_t d) {
+    const int64_t rr = j - 1, g = rr >> 7;
+    const int64_t big = (int64_t)SR * (SQ + 1);
+    const int64_t s = g < big ? g / (SQ + 1) : SR + (g - big) / SQ;
+    const int64_t g0 = s * SQ + (s < SR ? s : SR);
+    const int64_t r = rr - 128 * g0;
+    const int64_t base = ((i - 1) >> 12) << 12;
+    return (uint32_t)(r + (i - base)) * (uint32_t)d;
+}
+
 __device__ __forceinline__ int32_t score_at(const TableView& v, int64_t i, int64_t j) {
     if (i == 0) return (int32_t)(-(j + v.row_base) * (int64_t)v.d);
     if (j == 0) return v.top ? v.top[i - 1] + v.d : (int32_t)(-i * (int64_t)v.d);
-    return v.tiles[score_index(j - 1, i - 1, v.spitch, v.skew, v.pair)];
+    const int32_t x = v.tiles[score_index(j - 1, i - 1, v.spitch, v.skew, v.pair)];
+    return v.raw ? (int32_t)((uint32_t)x - raw_offset(i, j, v.SQ, v.SR, v.d)) : x;
 }
 
 // Direction code of cell (i, j).  A panel's row 0 belongs to the panel above

@@ -49,6 +49,11 @@ SHIFT_INTO_T = True
 # column) and the two symbol words in one ds_write2_b32: 11 LDS ops a block
 # instead of 16.
 RING2 = True
+# Timing-only experiments (wrong results; never the product): drop the two
+# cross-row prefix levels (row_bcast:15/31) and/or the score adds, to price
+# the chain against the issue count on the GPU (tools/ab_build_pair.sh).
+EXP_NO_BCAST = False
+EXP_NO_SCORES = False
 
 
 def GA(s):
@@ -116,20 +121,24 @@ def column_items(c, ST, HH=True, FF=True):
     its = ring_items(c)
     if not HH and not FF:
         return its
+    if EXP_NO_SCORES:
+        HH, ST = False, False
     if not FF:
         return its + [It("Hb", f"v_add3_u32 %[hb{c}], %[{GB(c)}], %[nlob], %[kd{c}]"),
                       It("Ha", f"v_add3_u32 %[ha{c}], %[{GA(c)}], %[nloa], %[kd{c}]", ["F"])]
     its = []
     # row b parts need no F
     its.append(It("Lb", f"v_sub_u32_e32 %[dLb], %[{GB(c - 1)}], %[{GB(c)}]"))
-    its.append(It("Hb", f"v_add3_u32 %[hb{c}], %[{GB(c)}], %[nlob], %[kd{c}]"))
+    if HH:
+        its.append(It("Hb", f"v_add3_u32 %[hb{c}], %[{GB(c)}], %[nlob], %[kd{c}]"))
     its += ring_items(c)
     its.append(It("Db", f"v_sub_u32_e32 %[dDb], %[{DGB(c)}], %[{GB(c)}]"))
     its.append(It("Ub", f"v_sub_u32_e32 %[dUb], %[{GA(c)}], %[{GB(c)}]", ["F"]))
     its.append(It("La", f"v_sub_u32_e32 %[dLa], %[{GA(c - 1)}], %[{GA(c)}]", ["F"]))
     its.append(It("Ua", f"v_sub_u32_e32 %[dUa], %[{SH(c + 1)}], %[{GA(c)}]", ["F"]))
     its.append(It("Da", f"v_sub_u32_e32 %[dDa], %[{DGA(c)}], %[{GA(c)}]", ["F"]))
-    its.append(It("Ha", f"v_add3_u32 %[ha{c}], %[{GA(c)}], %[nloa], %[kd{c}]", ["F"]))
+    if HH:
+        its.append(It("Ha", f"v_add3_u32 %[ha{c}], %[{GA(c)}], %[nloa], %[kd{c}]", ["F"]))
     hiA = "0" if c == 0 else "%[accA]"
     hiB = "0" if c == 0 else "%[accB]"
     its.append(It("bA1", f"v_alignbit_b32 %[accA], {hiA}, %[dLa], 31", ["La"]))
@@ -214,6 +223,8 @@ def block(ST, P, HH=True, FF=True):
         emit(It("A4", f"v_max3_i32 %[{GB(s)}], %[{GB(s - 1)}], %[{DGB(s)}], %[{XA(s)}]"))
         dpps = ["row_shr:1 row_mask:0xf", "row_shr:2 row_mask:0xf", "row_shr:4 row_mask:0xf",
                 "row_shr:8 row_mask:0xf", "row_bcast:15 row_mask:0xa", "row_bcast:31 row_mask:0xc"]
+        if EXP_NO_BCAST:
+            dpps = dpps[:4]
         g = GB(s)
         for dp in dpps:
             gap(pool)
@@ -323,7 +334,11 @@ def main():
     ap.add_argument("--out", default=OUT)
     ap.add_argument("--read-at", type=int, default=READ_AT)
     ap.add_argument("--align", type=int, choices=(0, 4), default=ALIGN)
+    ap.add_argument("--exp-no-bcast", action="store_true")
+    ap.add_argument("--exp-no-scores", action="store_true")
     args = ap.parse_args()
+    globals()["EXP_NO_BCAST"] = args.exp_no_bcast
+    globals()["EXP_NO_SCORES"] = args.exp_no_scores
     globals()["READ_AT"] = args.read_at
     globals()["ALIGN"] = args.align
     parts = ["// GENERATED by tools/gen_pair_asm.py -- do not edit; see the generator for the schedule.\n",
@@ -341,6 +356,26 @@ def main():
                 f"template <> __device__ __forceinline__ void pair_chunk_asm<{tf(HH)}, {tf(FF)}, {tf(ST)}, {tf(P)}>"
                 f"(PairRegs& r, const PairConst& k, PairSlot& ts, PairSlot& ns, int cv, int ra, int rd) {{\n"
                 f"{decl}    asm volatile(\n{cstr(lines)}\n{operands(chr(10).join(lines))}"
+                f"        : \"vcc\", \"memory\");\n}}\n")
+    # Raw-score blocks (nw_pair.hip, fills with scores and without stats): no
+    # H = G' + nlo + kd adds; the block's own G' registers of columns 0..6 are
+    # the score outputs (r.ha / r.hb; column 7 is r.ga / r.gb), and the
+    # readers add the affine offset back (nwk::raw_offset).
+    parts.append("template <bool FF, bool P>\n"
+                 "__device__ __forceinline__ void pair_chunk_raw(PairRegs& r, const PairConst& k, PairSlot& ts,\n"
+                 "                                               PairSlot& ns, int cv, int ra, int rd);\n")
+    for FF in (1, 0):
+        for P in (0, 1):
+            lines = block(0, P, False, bool(FF))
+            nvalu = sum(1 for x in lines if x.startswith("v_"))
+            ops = operands(chr(10).join(lines))
+            for q in range(7):
+                ops = ops.replace(f"(ga_[{q}])", f"(r.ha[{q}])").replace(f"(gb_[{q}])", f"(r.hb[{q}])")
+            parts.append(f"// VALU pair_chunk_raw<{tf(FF)}, {tf(P)}>: {nvalu} per 8 columns x 128 rows\n")
+            parts.append(
+                f"template <> __device__ __forceinline__ void pair_chunk_raw<{tf(FF)}, {tf(P)}>"
+                f"(PairRegs& r, const PairConst& k, PairSlot& ts, PairSlot& ns, int cv, int ra, int rd) {{\n"
+                f"{decl}    asm volatile(\n{cstr(lines)}\n{ops}"
                 f"        : \"vcc\", \"memory\");\n}}\n")
     with open(args.out, "w") as f:
         f.write("\n".join(parts))
