@@ -263,6 +263,17 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
                 if (lane == 0) __hip_atomic_store(&sh_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 cd = NC;
             }
+            // Everything per chunk but the slot read, one add and the store is
+            // scalar: the publisher shares a SIMD with a compute wave, and its
+            // vector instructions come out of that wave's issue
+            // (profiles/r02e_ab_chain_issue.txt; as nw_pair.hip).
+            cd = uni(cd);
+            const uint32_t tag = publish ? a.gtag | (uint32_t)(sidx + 1) : a.epoch;
+            gu64* const gdst = (gu64*)(publish ? gout : a.xout);
+            // (plain domain: H - d = G' - 128*nw*d - (i - base)d, i = CH*cd + lane + 1)
+            int nklane = -(64 * nw * d + (lane + 1) * d);
+            asm volatile("" : "+v"(nklane));                       // one v_add3 per granule
+            const int* const botl = bot + lane;
             while ((publish || xpublish) && cd < NC) {
                 const int p = uni(lds_ld(&ctr[2 * nw + 2]));          // prog of the last wave's ring
                 if (p <= cd) {
@@ -273,16 +284,15 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
                 lds_order();
                 for (; cd < p; ++cd) {
                     const int n = (cd == NC - 1) ? nlast : CH;
+                    const int nsv = -(CH * cd - chunk_base(cd)) * d;
+                    gu64* const gp = gdst + CH * (int64_t)cd;
                     if (lane < n) {
-                        // (plain domain: H - d = G' - 64*nw*d - (i - base)d)
-                        const int v = bot[(cd % R) * SLOT + lane] - 64 * nw * d - (CH * cd + lane + 1 - chunk_base(cd)) * d;
-                        const uint64_t tag = publish ? a.gtag | (uint32_t)(sidx + 1) : a.epoch;
-                        const uint64_t gr = (tag << 32) | (uint32_t)v;
-                        if (publish)
-                            put_granule(gout, CH * (int64_t)cd + lane, gr);
+                        const int v = botl[(cd % R) * SLOT] + nklane + nsv;
+                        const uint64_t gr = ((uint64_t)tag << 32) | (uint32_t)v;
+                        if (publish)   // put_granule (nw_kern.h) on the global address space
+                            __hip_atomic_store(gp + lane, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         else
-                            __hip_atomic_store(a.xout + CH * (int64_t)cd + lane, gr, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                            __hip_atomic_store(gp + lane, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     }
                     if (xpublish && a.xflag && ((cd + 1) % a.xblk == 0 || cd == NC - 1)) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the block is out before its flag
@@ -298,12 +308,12 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
             // ---------------- loader wave: no stores, exact waits ----------------
             // Source of the WG-stripe's top row: the seeded row 0, the panel
             // above (xin, written by another agent: system-scope loads), or
-            // the previous WG-stripe's granules (agent scope).  Lanes 8, 9
-            // write the chunk's top-string bytes.
+            // the previous WG-stripe's granules (agent scope).  Lanes 8k..8k+7
+            // write chunk cw + k's row above and its top-string words.
             // Nothing it waits for per chunk is a fresh global load unless the
             // granules are not there yet: the granule window (8 chunks, one lane
-            // per granule) and the top-string window (lanes 0..15: the 16 dwords
-            // of those 8 chunks) are prefetched one window ahead; a per-chunk
+            // per granule) and the top-string window (2 dwords per chunk) are
+            // prefetched one window ahead; a per-chunk
             // dependent load made the loader, not the producer, pace every
             // WG-stripe hop (+11% at 100k^2, tools/trace_lag.py).  Kept inline:
             // the same loop as a shared __device__ function compiled 5-10%
@@ -319,77 +329,99 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
                 const int64_t x = (int64_t)CH * cf + lane;
                 return x < ngr ? ld_gran(gin + x, xsrc) : 0ull;
             };
-            int cw = 0;
-            uint64_t pf = 0, pn = 0;
             const int64_t nsw = 2 * (int64_t)NC + 16;
+            // lanes 8k and 8k+1 hold the two symbol words of chunk cf + k
+            // (the other lanes duplicates), so the lanes that write chunk
+            // cf + k's row-above values write its symbols in the same ds_write2
             auto sload = [&](int cf) -> uint32_t {
-                const int64_t x = 2 * (int64_t)cf + lane;
-                return lane < 16 && x < nsw ? s1w[x] : 0u;
+                const int64_t x = 2 * (int64_t)cf + 2 * wk + (wb & 1);
+                return x < nsw ? s1w[x] : 0u;
             };
-            uint32_t sw = sload(0), swn = sload(CH);
-            if (!seeded) {
-                pf = gload(0);
-                pn = gload(CH);
-            }
-            for (int c = 0; c < NC; ++c) {
-                const int n = (c == NC - 1) ? nlast : CH;
-                if (c == cw + CH) {
-                    cw += CH;
-                    pf = pn;
-                    sw = swn;
-                    if (!seeded) pn = gload(cw + CH);
-                    swn = sload(cw + CH);
-                }
-                const bool tcm = NW_TRACE_EXT && a.trace && lane == 0 && c == trace_mid_chunk(NC, R);
-                if (tcm) *trace_ext(a, TX_REACH, sidx) = __builtin_amdgcn_s_memrealtime();
-                while (lds_ld(&ctr[1]) < c - R + 1) __builtin_amdgcn_s_sleep(1);
-                if (tcm) *trace_ext(a, TX_CREDIT, sidx) = __builtin_amdgcn_s_memrealtime();
-                int* dst = &tring[(c % R) * SLOT];
-                const int base = chunk_base(c);
-                if (seeded) {
-                    // row 0: H[i][0] - d = -(i+1)*d (computation.c:102-110) -> G' = -(base+1)*d
-                    if (lane < CH) dst[lane] = -(base + 1) * d;
-                } else {
-                    const bool mine = wk == c - cw;
-                    bool ok = !mine || wb >= n || (uint32_t)(pf >> 32) == want;
-                    if (!__all(ok)) {
-                        const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
-                        for (;;) {
+            // (H - d of the row above -> G' of row -1: + (i - base)*d, i = CH*c + wb + 1)
+            int kwb = (wb + 1) * d;
+            asm volatile("" : "+v"(kwb));
+            const int dst0 = lds_addr(tring) + 4 * wb;
+            // One window of CH chunks out of cur / scur, with the next window's
+            // granules and symbols prefetched into nxt / snxt.  The two windows'
+            // registers alternate (ping-pong, no copies): a copy of the
+            // prefetched value into the loop-carried register made the
+            // compiler wait for the prefetch right after issuing it, so every
+            // window shift stalled the loader for a full load latency.
+            auto window = [&](int cw, uint64_t& cur, uint64_t& nxt, uint32_t& scur, uint32_t& snxt) -> bool {
+                // this window's loads were issued a window ago: take them now,
+                // before the prefetch goes out, so no later wait covers it
+                asm volatile("" ::"v"(cur), "v"(scur));
+                if (!seeded) nxt = gload(cw + CH);
+                snxt = sload(cw + CH);
+                const int ce = min(cw + CH, NC);
+                for (int c = cw; c < ce; ++c) {
+                    const int n = (c == NC - 1) ? nlast : CH;
+                    const bool tcm = NW_TRACE_EXT && a.trace && lane == 0 && c == trace_mid_chunk(NC, R);
+                    if (tcm) *trace_ext(a, TX_REACH, sidx) = __builtin_amdgcn_s_memrealtime();
+                    if (uni(lds_ld(&ctr[1])) < c - R + 1) {                      // ring slot not free yet
+                        while (uni(lds_ld(&ctr[1])) < c - R + 1) {
+                            if (uni(lds_ld(&sh_abort))) break;
                             __builtin_amdgcn_s_sleep(1);
-                            if (wk >= c - cw && (uint32_t)(pf >> 32) != want) pf = gload(cw);
-                            ok = !mine || wb >= n || (uint32_t)(pf >> 32) == want;
-                            if (__all(ok)) break;
-                            const int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
-                            const uint32_t ab = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED,
-                                                                  __HIP_MEMORY_SCOPE_AGENT);
-                            const bool peer = xsrc && __any(mine && wb < n && (uint32_t)(pf >> 32) == (want | POISON_BIT));
-                            if (ab || peer || now - t0 > a.spin_ticks) {
-                                if (lane == 0) {
-                                    __hip_atomic_store(&a.ctl[CTL_ABORT], 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-                                    if (!ab)
-                                        atomicCAS(&a.ctl[CTL_ERR], 0u,
-                                                  (uint32_t)(peer ? NW_ERR_PEER : NW_ERR_TIMEOUT));
-                                    __hip_atomic_store(&sh_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                }
-                                break;
-                            }
                         }
+                        if (uni(lds_ld(&sh_abort))) return false;
                     }
-                    if (lds_ld(&sh_abort)) break;
-                    if (tcm) *trace_ext(a, TX_LOAD, sidx) = __builtin_amdgcn_s_memrealtime();
-                    // H - d of the row above -> G' of row -1: + (i - base)*d
-                    if (mine) dst[wb] = (int)(uint32_t)pf + (CH * c + wb + 1 - base) * d;
-                    if (xsrc && mine && wb < n) a.row0[CH * c + wb] = (int)(uint32_t)pf;
-                }
-                {
+                    if (tcm) *trace_ext(a, TX_CREDIT, sidx) = __builtin_amdgcn_s_memrealtime();
                     const int k = c - cw;
-                    const int b0 = __builtin_amdgcn_readlane((int)sw, 2 * k), b1 = __builtin_amdgcn_readlane((int)sw, 2 * k + 1);
-                    if (lane == 8) dst[8] = b0;
-                    if (lane == 9) dst[9] = b1;
+                    const bool mine = wk == k;                                  // lanes 8k .. 8k+7
+                    const int nbase = (CH * c - chunk_base(c)) * d;
+                    int v;
+                    if (seeded) {
+                        // row 0: H[i][0] - d = -(i+1)*d (computation.c:102-110) -> G' = -(base+1)*d
+                        v = -(chunk_base(c) + 1) * d;
+                    } else {
+                        // every granule of the chunk this loader needs carries the tag
+                        const uint64_t need = ((n == CH ? 0xffull : (1ull << n) - 1)) << (8 * k);
+                        if ((__ballot((uint32_t)(cur >> 32) == want) & need) != need) {
+                            const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+                            bool stop = false;
+                            for (;;) {
+                                __builtin_amdgcn_s_sleep(1);
+                                if (wk >= k && (uint32_t)(cur >> 32) != want) cur = gload(cw);
+                                if ((__ballot((uint32_t)(cur >> 32) == want) & need) == need) break;
+                                const int64_t now = (int64_t)__builtin_amdgcn_s_memrealtime();
+                                const uint32_t ab = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT);
+                                const bool peer = xsrc && __any(mine && wb < n && (uint32_t)(cur >> 32) == (want | POISON_BIT));
+                                if (ab || peer || now - t0 > a.spin_ticks) {
+                                    if (lane == 0) {
+                                        __hip_atomic_store(&a.ctl[CTL_ABORT], 1u, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+                                        if (!ab)
+                                            atomicCAS(&a.ctl[CTL_ERR], 0u,
+                                                      (uint32_t)(peer ? NW_ERR_PEER : NW_ERR_TIMEOUT));
+                                        __hip_atomic_store(&sh_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    }
+                                    stop = true;
+                                    break;
+                                }
+                            }
+                            if (stop) return false;
+                        }
+                        if (tcm) *trace_ext(a, TX_LOAD, sidx) = __builtin_amdgcn_s_memrealtime();
+                        v = (int)(uint32_t)cur + kwb + nbase;
+                        if (xsrc && mine && wb < n) a.row0[CH * c + wb] = (int)(uint32_t)cur;
+                    }
+                    // lanes 8k..8k+7: slot[wb] = the row above, slot[8 + wb] = symbol
+                    // word wb (wb < 2; the others land in the slot's unused tail)
+                    if (mine) {
+                        const int ad = dst0 + (c % R) * SLOT * 4;
+                        asm volatile("ds_write2_b32 %0, %1, %2 offset1:8" :: "v"(ad), "v"(v), "v"(scur) : "memory");
+                    }
+                    lds_order();
+                    if (lane == 0) lds_publish(&ctr[2], c + 1);
                 }
-                lds_order();
-                if (lane == 0) lds_publish(&ctr[2], c + 1);
+                return true;
+            };
+            uint64_t gA = seeded ? 0ull : gload(0), gB = 0;
+            uint32_t sA = sload(0), sB = 0;
+            for (int cw = 0; cw < NC; cw += 2 * CH) {
+                if (!window(cw, gA, gB, sA, sB)) break;
+                if (cw + CH < NC && !window(cw + CH, gB, gA, sB, sA)) break;
             }
             if (xsrc) xcredit_post(a);
         } else if (real) {

@@ -63,6 +63,7 @@ struct FillArgs {
 
 // ---------------------------------------------------------------- DPP helpers
 typedef const __attribute__((address_space(4))) uint64_t* cptr64;
+typedef __attribute__((address_space(1))) uint64_t gu64;   // global-address-space granule
 
 
 // LDS byte address of a __shared__ object (for ds_* in inline asm).

@@ -62,8 +62,6 @@ __device__ __forceinline__ void pair_store_scores(const int* h, int32_t* p) {
     __builtin_nontemporal_store(v4i{h[4], h[5], h[6], h[7]}, reinterpret_cast<v4i*>(p + 256));
 }
 
-typedef __attribute__((address_space(1))) uint64_t gu64;
-
 // Operands of the generated chunk block (nw_pair_chunk.inc).
 struct PairSlot {
     v4i a, b;           // T (row above, G') of columns 0..3, 4..7 of the chunk
@@ -221,8 +219,8 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
             // ---------------- loader wave: ring 0 (as the one-row kernel's) ----------------
             // Nothing it waits for per chunk is a fresh global load unless the
             // granules are not there yet: the granule window (8 chunks, one lane
-            // per granule) and the top-string window (lanes 0..15: the 16 dwords
-            // of those 8 chunks) are prefetched one window ahead; a per-chunk
+            // per granule) and the top-string window (2 dwords per chunk) are
+            // prefetched one window ahead; a per-chunk
             // dependent load made the loader, not the producer, pace every
             // WG-stripe hop (+11% at 100k^2, tools/trace_lag.py).  Kept inline:
             // the same loop as a shared __device__ function compiled 5-10%
