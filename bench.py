@@ -12,7 +12,7 @@ resident in HBM.  value = L1*L2 / ms_per_step in GCUPS (whole job).
          set) this process is one rank; run plainly, it starts N rank
          processes itself (before touching any GPU) and exits with their
          status.  The table is split into row panels across the ranks
-         (strong scaling of one table, bench_multi.py, DESIGN.md section 8).
+         (strong scaling of one table, bench_multi.py).
 
 Extra JSON fields:
   roofline     -- the fill kernel's algorithmic bytes (4.5 B/cell: 4 B score
@@ -23,12 +23,17 @@ Extra JSON fields:
                   this workload, with its source named.  Score-only fills
                   (--outputs '') are VALU-bound: int32 VALU lane-ops per cell
                   (from the generated block) x cells/s vs the int32 VALU peak.
-  parity       -- corner (and stats) of the timed table vs the committed
-                  fixture for this workload (tests/golden/), when one exists.
+  parity       -- the timed table vs the committed fixture for this workload
+                  (tests/golden/): its corner, and the whole table -- every
+                  score and direction code, hashed on the device after the
+                  timed loop (column-chained FNV-1a-64).
   cpu_baseline -- the reference itself (oracle/_ref/ref_harness: its own
                   compute_table_scores, compiled from its sources) on this
-                  host, serial and with -p threads, on config C2 (10k x 10k)
-                  -- a bounded sample; nproc and the CPU model are recorded.
+                  host: serial and -p 16 on config C2 (10k x 10k), -p $(nproc)
+                  on a smaller sample; fill phase alone and with the
+                  reference's allocation + seeding; each leg's rate scaled to
+                  100k x 100k (labelled extrapolated: the reference itself
+                  would need 1.36 TB there); nproc and the CPU model recorded.
   c2           -- config C2 on the GPU (10k x 10k, same fill) next to it.
 """
 import argparse
@@ -47,8 +52,16 @@ sys.path.insert(0, os.path.join(ROOT, "needleman-wunsch_amd"))
 import nw_amd  # noqa: E402  (the library itself loads lazily, on first use)
 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
-# int32 VALU peak: 256 CUs x 4 SIMDs x 16 lanes per clock x 2.4 GHz
-VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
+# int32 VALU peak of the chip: 256 CUs x 4 SIMDs, each SIMD 32 lanes per clock
+# (a wave64 VALU instruction issues over 2 cycles: MI355X_MICROARCH.md
+# "Wave scheduling"), at 2.4 GHz.
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# What the fill's own instruction mix can reach: its block is DPP, SDWA and
+# three-operand VOP3 instructions, which a SIMD issues at one per ~4.1-4.4
+# cycles whatever the wave count (tools/ubench_simd.hip,
+# profiles/r01_ubench_simd.txt) -- 64 lanes / 4.1 clk.  A property of this
+# code, reported beside the chip peak, not instead of it.
+VALU_MIX_TOPS = 256 * 4 * (64 / 4.1) * 2.4e9 / 1e12
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
@@ -62,9 +75,11 @@ def parse(argv=None):
     ap.add_argument("--mkd", type=int, nargs=3, default=(1, 1, 1))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c2", action="store_true", help="skip the 10k x 10k GPU line")
+    ap.add_argument("--no-hash", action="store_true",
+                    help="skip the whole-table hash of the timed table (A/B timing runs only)")
     ap.add_argument("--outputs", default="sd",
                     help="what the fill writes: s = scores, d = direction codes, t = stats "
-                         "('' = score-only); the metric's workload is 'sd'")
+                         "('' or 'none' = score-only); the metric's workload is 'sd'")
     ap.add_argument("--cpu-sample", type=int, default=10_000,
                     help="side of the square sample the CPU reference fills (config C2: 10k)")
     ap.add_argument("--cpu-threads", type=int, default=16,
@@ -76,7 +91,10 @@ def parse(argv=None):
                          "several ranks on one GPU)")
     ap.add_argument("--device", type=int, default=None,
                     help="N > 1: force every rank onto this device (rehearsal on one GPU)")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.outputs in ("none", "-"):
+        a.outputs = ""
+    return a
 
 
 def mask_of(outputs):
@@ -118,7 +136,10 @@ def fixture_for(L1, L2, mkd):
 
 
 def parity(L1, L2, mkd, stats):
-    """Compare the timed table's corner (and stats when computed) with the fixture."""
+    """Compare the timed table with the fixture: the corner, the stats when
+    computed, and -- when the table was hashed (stats["hH2"] / ["hD2"], the
+    column-chained FNV-1a-64 of every score and every direction code, computed
+    on the device after the timed loop) -- the whole table."""
     fx = fixture_for(L1, L2, mkd)
     if fx is None:
         return {"fixture": None, "corner": stats.get("corner")}
@@ -129,6 +150,11 @@ def parity(L1, L2, mkd, stats):
         out["gav_ok"] = stats["gav"] == r["gav"]
         out["branch_count_ok"] = stats["bc"] == r.get("branch_count", r.get("bc"))
         out["ok"] = out["ok"] and out["gav_ok"] and out["branch_count_ok"]
+    for key in ("hH2", "hD2"):
+        if stats.get(key) is not None and key in r:
+            out[key] = stats[key]
+            out[key + "_ok"] = stats[key] == r[key]
+            out["ok"] = out["ok"] and out[key + "_ok"]
     return out
 
 
@@ -172,7 +198,10 @@ def roofline(L1, L2, outputs, kern_ms):
                 "unit": "T int32 ops/s", "frac": round(ach / VALU_PEAK_TOPS, 4) if ach else None,
                 "ops_per_cell": ops, "traffic": None, "kernel_ms": round(kern_ms, 4),
                 "kernel_gcups": round(cells / (kern_ms * 1e-3) / 1e9, 2),
-                "note": "score-only: no table stream; the stripe chain's issue rate binds (DESIGN.md section 4)"}
+                "mix_ceiling": {"peak": round(VALU_MIX_TOPS, 2), "frac": round(ach / VALU_MIX_TOPS, 4) if ach else None,
+                                "what": "issue rate of this block's DPP/SDWA/VOP3 mix (one instruction per "
+                                        "~4.1 SIMD cycles, measured); not the chip's peak"},
+                "note": "score-only: no table stream; peak = 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz"}
     alg = bpc * (L1 + 1) * (L2 + 1)
     ach = alg / (kern_ms * 1e-3) / 1e9
     tr = latest_traffic(L1, L2, outputs)
@@ -196,34 +225,62 @@ def cpu_model():
     return None
 
 
-def run_ref(n, T):
+def run_ref(n, T, timeout=900):
+    """One run of the compiled reference on an n x n sample with T threads:
+    {"init_s": alloc + seeding, "fill_s": compute_table_scores, "corner": ...} or None."""
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
-    out = subprocess.run([harness, "gen", str(n), str(n), "1", "1", "1", str(T)], capture_output=True, text=True,
-                         timeout=900)
+    try:
+        out = subprocess.run([harness, "gen", str(n), str(n), "1", "1", "1", str(T)], capture_output=True, text=True,
+                             timeout=timeout, env=dict(os.environ, NW_REF_TIME_ONLY="1"))
+    except subprocess.TimeoutExpired:
+        return {"timeout_s": timeout}
     if out.returncode != 0:
         return None
     return json.loads(out.stdout)
 
 
-def cpu_baseline(n, threads):
-    """The reference's own fill (serial, then -p threads) on an n x n sample on this host."""
+def _leg(n, r, what):
+    tot = r["init_s"] + r["fill_s"]
+    return {"value": round(n * n / r["fill_s"] / 1e9, 5), "unit": "GCUPS",
+            "value_with_alloc_seed": round(n * n / tot / 1e9, 5),
+            "fill_s": round(r["fill_s"], 3), "alloc_seed_s": round(r["init_s"], 3),
+            # The reference needs 136 B per cell: 1.36 TB at 100k x 100k, so it
+            # cannot run there; its rate on the sample, scaled by the cell count.
+            "extrapolated_100k_s": round(1e10 / (n * n) * tot, 1),
+            "sample": f"{n}x{n} random DNA, m=k=d=1, {what}: alloc+seed {r['init_s']:.2f} s, "
+                      f"fill {r['fill_s']:.2f} s; corner {r['corner']}"}
+
+
+def cpu_baseline(n, threads, n_all=3000):
+    """The reference's own fill on this host's cores, on bounded samples:
+    serial and `-p threads` on an n x n table (config C2 when n = 10k), and
+    `-p $(nproc)` -- what configs[1] names -- on an n_all x n_all table (every
+    thread of that leg blocks on a per-cell condition variable,
+    needleman-wunsch.c:444-475, so it is the slowest leg by far and gets the
+    smallest sample).  `value` is the fill phase alone, like the GPU line;
+    `value_with_alloc_seed` adds the reference's allocation and seeding, which
+    under -p initialises a mutex and a condition variable per cell
+    (computation.c:80-89)."""
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     nproc = os.cpu_count() or 1
     if os.path.exists(harness):
         r = run_ref(n, 1)
-        if r is not None:
-            res = {"value": round(n * n / r["fill_s"] / 1e9, 5), "unit": "GCUPS", "cores": 1, "kind": "reference",
-                   "sample": f"{n}x{n} random DNA (config C2), m=k=d=1: the reference's compute_table_scores "
-                             f"(needleman-wunsch.c:583, serial, -O3 -DNDEBUG) fill phase {r['fill_s']:.2f} s, "
-                             f"tables calloc'd cold as in the reference; corner {r['corner']}",
-                   "nproc": nproc, "cpu_model": cpu_model()}
-            # The reference's -p path (per-cell mutex/cond hand-off, needleman-wunsch.c:444-475).
+        if r is not None and "fill_s" in r:
+            res = _leg(n, r, "the reference's compute_table_scores (needleman-wunsch.c:583, serial, "
+                             "-O3 -DNDEBUG), tables calloc'd cold as in the reference")
+            res.update(cores=1, kind="reference", nproc=nproc, cpu_model=cpu_model())
             T = max(2, min(threads, nproc))
             rp = run_ref(n, T)
-            if rp is not None:
-                res["pthread"] = {"value": round(n * n / rp["fill_s"] / 1e9, 5), "unit": "GCUPS", "threads": T,
-                                  "sample": f"{n}x{n}, -p {T} (nproc {nproc}; {T} = this GPU's CPU share): "
-                                            f"fill phase {rp['fill_s']:.2f} s; corner {rp['corner']}"}
+            if rp is not None and "fill_s" in rp:
+                res["pthread"] = dict(_leg(n, rp, f"-p {T} (this GPU's CPU share of the host's {nproc})"), threads=T)
+            if nproc > T:
+                ra = run_ref(n_all, nproc, timeout=150)
+                if ra is not None and "fill_s" in ra:
+                    res["pthread_nproc"] = dict(_leg(n_all, ra, f"-p {nproc} = -p $(nproc), configs[1]'s CPU leg, on "
+                                                                f"a smaller sample to bound the run"), threads=nproc)
+                elif ra is not None:
+                    res["pthread_nproc"] = {"threads": nproc, "value": None,
+                                            "sample": f"{n_all}x{n_all}, -p {nproc}: not finished in {ra['timeout_s']} s"}
             return res
     # Fallback: the clean-room restatement (same algorithm, dense layout).
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -233,12 +290,12 @@ def cpu_baseline(n, threads):
     O.fill(s1, s2, 1, 1, 1)
     dt = time.perf_counter() - t0
     return {"value": round(n * n / dt / 1e9, 5), "unit": "GCUPS", "cores": 1, "kind": "port", "nproc": nproc,
-            "cpu_model": cpu_model(),
+            "cpu_model": cpu_model(), "extrapolated_100k_s": round(1e10 / (n * n) * dt, 1),
             "sample": f"{n}x{n} random DNA, m=k=d=1: oracle/nw_oracle.c serial fill {dt:.2f} s"}
 
 
 # ---------------------------------------------------------------- single GPU
-def time_fills(L1, L2, mkd, outputs, steps, warmup):
+def time_fills(L1, L2, mkd, outputs, steps, warmup, hash_table=True):
     m, k, d = mkd
     mask = mask_of(outputs)
     with nw_amd.Table(L1, L2, mask | nw_amd.NW_OUT_STATS) as t:
@@ -255,12 +312,19 @@ def time_fills(L1, L2, mkd, outputs, steps, warmup):
         stats = {"corner": st.corner}
         if "t" in outputs:
             stats.update(gav=st.greatest_abs_interior, bc=st.branch_count)
+        # Outside the timed region: the table the last timed step left in HBM,
+        # hashed on the device (every score; every direction code when written).
+        if "s" in outputs and hash_table:
+            hH, hD = t.hash()
+            stats["hH2"] = "%016x" % hH
+            if "d" in outputs:
+                stats["hD2"] = "%016x" % hD
         return dt, kern, t.waves, stats
 
 
 def run_single(a):
     L1, L2 = a.L1, a.L2
-    dt, kern, waves, stats = time_fills(L1, L2, a.mkd, a.outputs, a.steps, a.warmup)
+    dt, kern, waves, stats = time_fills(L1, L2, a.mkd, a.outputs, a.steps, a.warmup, not a.no_hash)
     ms = dt / a.steps * 1e3
     kern_ms = sum(kern) / len(kern)
     out = {
@@ -274,7 +338,7 @@ def run_single(a):
         "parity": parity(L1, L2, tuple(a.mkd), stats),
     }
     if not a.no_c2 and (L1, L2) != (10_000, 10_000):
-        dt2, kern2, _, st2 = time_fills(10_000, 10_000, (1, 1, 1), "sd", 20, 5)
+        dt2, kern2, _, st2 = time_fills(10_000, 10_000, (1, 1, 1), "sd", 20, 5, not a.no_hash)
         ms2 = dt2 / 20 * 1e3
         out["c2"] = {"workload": workload_name(10_000, 10_000, "sd", (1, 1, 1)), "gcups": round(1e8 / (ms2 * 1e-3) / 1e9, 2),
                      "ms_per_step": round(ms2, 4), "kernel_ms": round(sum(kern2) / len(kern2), 4),

@@ -65,6 +65,25 @@ def max_over_ranks(x: float, group=None) -> float:
                for r in exchange_bytes(np.float64(x).tobytes(), group))
 
 
+def chain_hash_states(panel, L1: int, rank: int, world: int, group=None):
+    """Whole-table parity across ranks: the per-column FNV states travel down
+    the panel chain (rank r continues them over its own rows and hands them to
+    rank r + 1; CPU tensors over gloo).  Every rank returns the folded
+    (hH, hD) of the whole table."""
+    import torch
+    import torch.distributed as dist
+    state = nw_amd.hash_states(L1)
+    buf = torch.from_numpy(state.view(np.int64))
+    if rank > 0:
+        dist.recv(buf, src=rank - 1, group=group)
+    panel.hash_columns(state)
+    if rank + 1 < world:
+        dist.send(buf, dst=rank + 1, group=group)
+    out = [nw_amd.hash_fold(state) if rank == world - 1 else None]
+    dist.broadcast_object_list(out, src=world - 1, group=group)
+    return out[0]
+
+
 def make_panel(transport: str, rank: int, world: int, device: int, L1: int, L2: int, mask: int, group=None):
     """Create + connect this rank's panel (collective)."""
     kind = TRANSPORTS[transport]
@@ -120,6 +139,12 @@ def main(a) -> None:
     kern_ms = float(np.mean(kern)) if kern else 0.0
     per_rank = exchange_bytes(json.dumps({"rank": rank, "rows": rows, "kernel_ms": kern_ms,
                                           "waves": p.table.waves}).encode(), ctl)
+    # Outside the timed region: the table the last timed step left in the
+    # ranks' HBM, hashed on the devices panel by panel (every score; every
+    # direction code when written).
+    hashes = None
+    if "s" in a.outputs and rc == 0 and not getattr(a, "no_hash", False):
+        hashes = chain_hash_states(p, L1, rank, world, ctl)
     p.close()
     if rank == 0:
         info = [json.loads(x) for x in per_rank]
@@ -131,6 +156,20 @@ def main(a) -> None:
         alg = bpc * (L1 + 1) * (slow["rows"] + 1)
         achieved = alg / (slow["kernel_ms"] * 1e-3) / 1e9 if slow["kernel_ms"] > 0 else 0.0
         import bench
+        stats = {"corner": st.corner}
+        if "t" in a.outputs:
+            stats.update(gav=st.greatest_abs_interior, bc=st.branch_count)
+        if hashes is not None:
+            stats["hH2"] = "%016x" % hashes[0]
+            if "d" in a.outputs:
+                stats["hD2"] = "%016x" % hashes[1]
+
+        def rank_roofline(r):
+            alg_r = bpc * (L1 + 1) * (r["rows"] + (1 if r["rank"] == 0 else 0))
+            ach = alg_r / (r["kernel_ms"] * 1e-3) / 1e9 if r["kernel_ms"] > 0 else 0.0
+            return {"rank": r["rank"], "rows": r["rows"], "kernel_ms": round(r["kernel_ms"], 4),
+                    "waves_per_wg": r["waves"], "achieved_gbs": round(ach, 1),
+                    "frac": round(ach / HBM_PEAK_GBS, 4)}
         out = {
             "metric": bench.metric_name(L1, L2),
             "value": round(value, 2), "unit": "GCUPS", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -139,13 +178,12 @@ def main(a) -> None:
             "config": {"workload": bench.workload_name(L1, L2, a.outputs, (m, k, d)),
                        "L1": L1, "L2": L2, "parallelism": f"row panels x{world} ({transport})",
                        "corner": st.corner, "status": rc,
-                       "panels": [{"rank": r["rank"], "rows": r["rows"], "kernel_ms": round(r["kernel_ms"], 4),
-                                   "waves_per_wg": r["waves"]} for r in info]},
+                       "panels": [rank_roofline(r) for r in info]},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "bytes_per_cell": bpc, "traffic": None,
                          "kernel_ms": round(slow["kernel_ms"], 4), "alg_bytes_per_launch": alg,
                          "kernel_rank": slow["rank"]},
-            "parity": dict(bench.parity(L1, L2, (m, k, d), {"corner": st.corner}), status=rc),
+            "parity": dict(bench.parity(L1, L2, (m, k, d), stats), status=rc),
             "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)

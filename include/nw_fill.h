@@ -90,18 +90,36 @@ int nw_fill(const char *s1, int64_t L1, const char *s2, int64_t L2,
 /* ---------------------------------------------------------------------------
  * Device-resident table (the 100k x 100k path: the 45 GB table stays in HBM).
  *
- * Device layout (DESIGN.md "Data layout in HBM"):
- *   scores: stripe quad tiles.  Row 0 and column 0 (the seeds -i*d,
- *           -j*d) are not stored.  Interior cell (i, j) has stripe
- *           g = (j-1)/64, lane l = (j-1)%64, quad u = (i-1)/4, r = (i-1)%4
- *           and is element g*P + (u*64 + l)*4 + r with
+ * Device layout (for zero-copy consumers; everyone else uses the copy, hash
+ * and walk entry points below, which decode it).  Which variant a fill left
+ * in the table is reported by nw_table_layout(); the three fill kernels
+ * (column scan, skewed stripes, two rows per lane -- chosen per shape, or by
+ * $NW_KERNEL) share the tiling and differ in how a cell's row r = j - 1 and
+ * column q = i - 1 map into it:
+ *   rr = pair ? 64*(2*(r/128) + r%2) + (r%128)/2 : r     (two rows per lane)
+ *   t  = skew ? q + rr%64 : q                            (stored by step)
+ *   scores: stripe quad tiles.  Row 0 and column 0 (the seeds -i*d, -j*d) are
+ *           not stored.  Interior cell (i, j) is element
+ *             (rr/64)*P + ((t/4)*64 + rr%64)*4 + t%4,
  *           P = nw_table_score_pitch() = 512*NQ: a lane's 4 consecutive
  *           columns are 16 contiguous bytes, 8 columns of a stripe 2 KB.
- *   dirs  : 32-bit words, one per (64-row stripe g, 8-column group q, lane l):
- *           word (g*(NQ+1) + q + 1)*64 + l, NQ = ceil(L1/8) (row 0 of each
- *           stripe is padding), holds the codes of cells (i = 8q+1+s,
- *           j = 64g+1+l), s = 0..7, 3 bits each: code s in bits [21-3s, 23-3s]
- *           (bits 24..31 are 0).
+ *   dirs  : 32-bit words, one per (64-row stripe g = rr/64, 8-column group,
+ *           lane l = rr%64): word (g*(NQ+1) + t/8 + 1)*64 + l (row 0 of each
+ *           stripe is padding) holds 8 codes of 3 bits, code of t%8 = s in bits
+ *           [21-3s, 23-3s] (bits 24..31 are 0).
+ *           NQ = 8-column groups per stripe of the layout (nw_layout.NQ).
+ *   raw scores.  A fill with NW_OUT_SCORES and without NW_OUT_STATS that the
+ *           two-rows-per-lane kernel ran (nw_layout.raw = 1; the 100k x 100k
+ *           default) leaves the kernel's own shifted values in the tiles,
+ *             G' = H + rw*d + (i - base)*d   (mod 2^32),
+ *           rw = the row's offset inside its workgroup stripe, base = the
+ *           first column of the cell's 4096-column group:
+ *             g  = r/128;  big = SR*(SQ+1)
+ *             s  = g < big ? g/(SQ+1) : SR + (g - big)/SQ
+ *             rw = r - 128*(s*SQ + min(s, SR));  base = ((i-1)/4096)*4096
+ *             H  = G' - (rw + i - base)*d
+ *           with SQ, SR, d from nw_layout (the fill's stripe plan and indel
+ *           penalty).  Every entry point below returns H, never G'.
  */
 typedef struct nw_table nw_table;
 
@@ -127,7 +145,7 @@ int nw_table_stats(nw_table *t, nw_stats *st);
  * stream. */
 int nw_table_elapsed_ms(nw_table *t, float *fill_kernel_ms, float *fill_call_ms);
 /* Column-chained FNV-1a-64 of the scores and of the direction codes
- * (DESIGN.md "Parity hashes"): hH = FNV over the 8-byte LE FNV-1a-64 of each
+ * hH = FNV over the 8-byte LE FNV-1a-64 of each
  * column's int32 LE scores, i = 0..L1; hD likewise over one code byte per
  * cell.  Computed on the device. */
 int nw_table_hash(nw_table *t, uint64_t *hH, uint64_t *hD);
@@ -162,8 +180,24 @@ void nw_host_free(void *p);
  * nw_table_copy_codes / nw_table_copy_last_column).  Any pointer may be NULL. */
 int nw_table_io_stats(nw_table *t, double *upload_ms, int64_t *upload_bytes, double *copy_ms,
                       int64_t *copy_bytes);
-/* Geometry of the device layout (for zero-copy consumers). */
+/* Geometry of the device layout (for zero-copy consumers): the layout
+ * section above.  nw_table_layout fills *out for the last completed fill
+ * (NW_ERR_STATE before one). */
+typedef struct nw_layout {
+        int64_t score_pitch;   /* P: int32 elements per 64-row stripe           */
+        int64_t NQ;            /* 8-column groups per stripe                     */
+        int32_t pair;          /* rows permuted (two-rows-per-lane kernel)       */
+        int32_t skew;          /* stored by step (skewed-stripe kernel)          */
+        int32_t raw;           /* score tiles hold G', see "raw scores"          */
+        int32_t SQ, SR;        /* raw: the fill's workgroup-stripe plan          */
+        int32_t d;             /* raw: the fill's indel penalty                  */
+        int32_t has_scores, has_dirs;
+} nw_layout;
 int64_t nw_table_score_pitch(const nw_table *t);
+int nw_table_layout(const nw_table *t, nw_layout *out);
+/* Device pointers of the score tiles and code words (NULL when not
+ * allocated).  They stay valid until nw_table_destroy. */
+int nw_table_device_buffers(const nw_table *t, const int32_t **scores, const uint32_t **dirs);
 /* In-kernel timeline of the last fill, recorded only when $NW_TRACE is set:
  * 8 words per workgroup stripe s -- s_memrealtime (100 MHz) at [8s] dequeue,
  * [8s+1] first wave started, [8s+2] last wave finished; [8s+3] blockIdx |
@@ -221,7 +255,7 @@ int nw_table_enumerate_paths(nw_table *t, uint64_t first, uint64_t count, uint8_
  * bottom-up and walked greedily (needleman-wunsch.c:296-322), each only left
  * of where the walk entered it.  Device memory ~ band_rows * L1 / 2 bytes +
  * 8 * L1 per band; time ~ two fills.  Not in the reference (its traceback
- * needs every cell's walk state, walk-table.c:58-79); SURVEY.md 8(f) item 3.
+ * needs every cell's walk state, walk-table.c:58-79).
  * device: as nw_fill; cap >= L1 + L2; moves as nw_table_first_path. */
 int nw_first_path_banded(int device, const char *s1, int64_t L1, const char *s2, int64_t L2,
                          int32_t m, int32_t k, int32_t d, int64_t band_rows,

@@ -7,7 +7,7 @@
  * contiguous ROW panels: panel r holds global rows row_base+1 .. row_base+rows
  * (whole 128-row stripes; every panel but the last has a multiple of 128 rows,
  * so every feeding panel can run the two-rows-per-lane kernel)
- * for all columns.  This is SURVEY.md section 8(e)'s column-panel scheme
+ * for all columns.  This is the column-panel scheme
  * transposed to this fill's stripe orientation (waves sweep columns): the
  * exchange is the single boundary ROW, in blocks of columns, and a panel
  * starts as soon as the first block of the row above it is done.
@@ -135,6 +135,17 @@ int nw_panel_set_sequences(nw_panel *p, const char *s1, int64_t L1, const char *
 /* IPC / RCCL: every rank calls it once per fill, same arguments.  Returns
  * this rank's status; a failure upstream surfaces as NW_ERR_PEER. */
 int nw_panel_fill(nw_panel *p, int32_t m, int32_t k, int32_t d, uint32_t out_mask);
+
+/* Back-pressure of the IPC / group transports.  A panel that receives a row
+ * posts "read" into a credit word (the fill's epoch) and the panel above
+ * waits for it before it overwrites that row in its next fill.  The credit
+ * is posted on every path -- by the kernel once it has read the row, by the
+ * host when the fill failed or never launched -- and the wait accepts the
+ * awaited epoch or any later one, so a failed panel costs the panel above no
+ * watchdog time-out on the next fill.  nw_panel_credit_reached is that
+ * comparison (epochs run 1 .. 2^31-1 and wrap to 1): 1 when `credit` is at
+ * or after `want`. */
+int nw_panel_credit_reached(uint32_t credit, uint32_t want);
 
 /* In-process group: fills all n panels of the group, in rank order. */
 int nw_panel_group_fill(nw_panel *const *ps, int n, int32_t m, int32_t k, int32_t d, uint32_t out_mask);

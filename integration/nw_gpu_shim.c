@@ -2,7 +2,7 @@
  * nw_gpu_shim.c -- the reference program's fill, moved to the MI355X.
  *
  * What a maintainer of skotchandsoda/needleman-wunsch adds to use this
- * build's fill (INTEGRATION.md): compute_table_scores_gpu() has the
+ * build's fill: compute_table_scores_gpu() has the
  * signature and the postconditions of the reference's hot path,
  *
  *     void compute_table_scores(computation_t *C);   needleman-wunsch.c:583-626

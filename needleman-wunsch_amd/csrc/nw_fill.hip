@@ -4,8 +4,7 @@
 // (needleman-wunsch.c:583-626 -> score_cell_column_set :557-574 ->
 // score_cell_column :523-543 -> score_cell :418-510 -> max3 :395-404) and the
 // table storage/seeding it relies on (score-table.c:60-81,
-// walk-table.c:58-79, computation.c:75-125).  See DESIGN.md for the full
-// derivation; in short:
+// walk-table.c:58-79, computation.c:75-125).  In short:
 //
 //  * A wave owns a 64-row stripe (lane l <-> row j0+l) and walks the columns
 //    i = 1..L1.  All 64 lanes compute the SAME column per step, so the
@@ -54,7 +53,7 @@ using namespace nwk;
 // the workgroup (64*w + lane), i = column, base = the column where the current
 // 4096-column "super-chunk" starts.  In it the left candidate H[i-1][j] - d is
 // G'_{i-1} itself, the diagonal is wave_shr1(G'_{i-1}) + sub + 2d, and the up
-// dependency becomes a prefix max over the lanes (DESIGN.md "Fill kernel"):
+// dependency becomes a prefix max over the lanes:
 //     G'_i = prefmax( max3(G'_{i-1}, wave_shr1(G'_{i-1}) + sub'_i, T'_i) ),
 //     sub' = match ? m + 2d : 2d - k,   T'_i = the row above, same domain.
 // base moves every 512 chunks so |G'| stays within |H| + (64W + 4104)|d|.
@@ -756,7 +755,7 @@ double host_ms() {
 }
 
 // ---------------------------------------------------------------- Host I/O
-// Streamed slice copies (SURVEY.md 8(f) item 2).  A slice of columns [i0, i1)
+// Streamed slice copies.  A slice of columns [i0, i1)
 // is gathered into dense column blocks of <= kStageBytes by a kernel on the
 // table's stream, alternating between two device staging buffers, while the
 // copy stream DMAs the previous block out: into the destination itself when
@@ -928,7 +927,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         // ~1.2 us per stripe, so the skew kernel wins only on very wide tables
         // with few stripes (measured: 1M x 20k 61 vs 75 ms, 100k x 64 4.6 vs
         // 6.2 ms; 100k x 12.5k 8.0 vs 7.0 ms and 100k x 100k 22 vs 11 ms the
-        // other way; DESIGN.md).  $NW_KERNEL = scan | skew | pair | auto (default).
+        // other way).  $NW_KERNEL = scan | skew | pair | auto (default).
         const char* ke = getenv("NW_KERNEL");
         if (ke && std::strcmp(ke, "skew") == 0) skew = true;
         else if (ke && std::strcmp(ke, "scan") == 0) skew = false;
@@ -1219,7 +1218,7 @@ int nw_table_create(int device, int64_t max_L1, int64_t max_L2, uint32_t out_mas
     }
     if ((rc = alloc((void**)&t->lastcol, (size_t)(64 * NG + 128) * 4))) return bail(rc);
     if ((rc = alloc((void**)&t->row0, (size_t)(max_L1 + 8) * 4))) return bail(rc);
-    // Granule slots: one per concurrently running WG-stripe + 1 (see DESIGN.md).
+    // Granule slots: one per concurrently running WG-stripe + 1.
     const int64_t gpitch = CH * NC + CH;
     const int64_t nslot = kMaxWgPerCu * (int64_t)t->ncu + 1;
     t->gran_bytes = (size_t)(gpitch * nslot * 8);
@@ -1316,6 +1315,31 @@ int64_t nw_table_trace(nw_table* t, uint64_t* dst, int64_t n) {
 }
 
 int64_t nw_table_score_pitch(const nw_table* t) { return t ? t->spitch : 0; }
+
+int nw_table_layout(const nw_table* t, nw_layout* out) {
+    if (!t || !out) return fail(NW_ERR_ARG, "nw_table_layout: NULL argument");
+    if (!t->filled) return fail(NW_ERR_STATE, "nw_table_layout: no completed fill");
+    nw_layout l{};
+    l.score_pitch = t->spitch;
+    l.NQ = t->lay_NC;
+    l.pair = t->pair;
+    l.skew = t->skew;
+    l.raw = t->raw;
+    l.SQ = t->SQ;
+    l.SR = t->SR;
+    l.d = t->last_d;
+    l.has_scores = (t->last_mask & NW_OUT_SCORES) != 0;
+    l.has_dirs = (t->last_mask & NW_OUT_DIRS) != 0;
+    *out = l;
+    return NW_OK;
+}
+
+int nw_table_device_buffers(const nw_table* t, const int32_t** scores, const uint32_t** dirs) {
+    if (!t) return fail(NW_ERR_ARG, "nw_table_device_buffers: NULL table");
+    if (scores) *scores = t->H;
+    if (dirs) *dirs = t->D;
+    return NW_OK;
+}
 int nw_table_waves(const nw_table* t) { return t ? t->waves : 0; }
 
 static int copy_scores_impl(nw_table* t, int64_t i0, int64_t i1, int32_t* dst) {

@@ -106,16 +106,25 @@ __device__ __forceinline__ uint64_t ld_gran(const uint64_t* p, bool sys) {
                : __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Epochs run 1 .. 2^31 - 1 and wrap to 1 (bit 31 is the poison bit); c is "at
+// or after" want when it is less than half the ring ahead of it.
+__host__ __device__ __forceinline__ bool epoch_reached(uint32_t c, uint32_t want) {
+    return ((c - want) & 0x7fffffffu) < 0x40000000u;
+}
+
 // Producer side of the panel back-pressure (FillArgs.xout_credit): one wave
-// waits until the consumer has read the previous fill's boundary row.  False
-// when the fill is being aborted (another wave's failure, or this wait's
-// watchdog: NW_ERR_TIMEOUT).
+// waits until the consumer has read the previous fill's boundary row, i.e.
+// until its credit word reads that fill's epoch or a later one (a consumer
+// whose fill failed or never launched posts its credit from the host, so
+// one failed panel does not stall its producer's next fill).  False when the
+// fill is being aborted (another wave's failure, or this wait's watchdog:
+// NW_ERR_TIMEOUT).
 __device__ __forceinline__ bool xcredit_wait(const FillArgs& a, const int* sh_abort) {
     if (!a.xout_credit) return true;
     const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
     for (;;) {
         const uint32_t c = __hip_atomic_load(a.xout_credit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (__builtin_amdgcn_readfirstlane((int)c) == (int)a.credit_want) return true;
+        if (epoch_reached((uint32_t)__builtin_amdgcn_readfirstlane((int)c), a.credit_want)) return true;
         const uint32_t ab = __hip_atomic_load(&a.ctl[CTL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (ab || __hip_atomic_load(sh_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
         if ((int64_t)__builtin_amdgcn_s_memrealtime() - t0 > a.spin_ticks) {

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "nw_internal.h"
+#include "nw_kern.h"
 #include "nw_panel.h"
 
 using nwi::fail;
@@ -157,14 +158,20 @@ void configure(nw_panel* p, uint32_t epoch, uint32_t prev_epoch) {
     }
 }
 
-// Every panel posts its credit for every fill: a fill kernel that reads the
-// row above posts it itself once read (xcredit_post); otherwise it is posted
-// here, stream-ordered after this panel's work, so a producer never waits on
-// a panel that has nothing to read (first panel, empty panel, L1 == 0).
-int post_credit(nw_panel* p, bool kernel_posts) {
-    if (p->transport == NW_PANEL_RCCL || kernel_posts) return NW_OK;
+// Every panel posts its credit for every fill, on every path: a fill kernel
+// that reads the row above posts it itself once read (xcredit_post);
+// otherwise it is posted here, stream-ordered after this panel's work, so a
+// producer never waits on a panel that has nothing to read (first panel,
+// empty panel, L1 == 0) -- or that failed: a fill that did not launch, or
+// whose kernel ended before its loader ran, gets its credit from here as
+// well (`failed`: on the send stream and waited for, since the fill's own
+// stream may be the thing that broke).  Posting an epoch twice is harmless.
+int post_credit(nw_panel* p, bool kernel_posts, bool failed = false) {
+    if (p->transport == NW_PANEL_RCCL || (kernel_posts && !failed)) return NW_OK;
     NW_HIPCHK(hipSetDevice(p->device));
-    NW_HIPCHK(hipMemsetD32Async(credit_of(p->xin, p->xcap), (int)p->epoch, 1, p->t->stream));
+    hipStream_t s = failed ? p->s_send : p->t->stream;
+    NW_HIPCHK(hipMemsetD32Async(credit_of(p->xin, p->xcap), (int)p->epoch, 1, s));
+    if (failed) NW_HIPCHK(hipStreamSynchronize(s));
     return NW_OK;
 }
 
@@ -474,6 +481,7 @@ int nw_panel_fill(nw_panel* p, int32_t m, int32_t k, int32_t d, uint32_t out_mas
         launched = rc == NW_OK;
     }
     if (rc == NW_OK) rc = post_credit(p, launched && t->xin);
+    else (void)post_credit(p, false, true);
     const int64_t NC = cdiv(p->L1, kChunk);
     const int64_t NB = (p->rows > 0 && p->L1 > 0) ? cdiv(NC, p->xblk) : 0;
     int xrc = NW_OK;   // transport failure (reported after the local fill)
@@ -482,7 +490,10 @@ int nw_panel_fill(nw_panel* p, int32_t m, int32_t k, int32_t d, uint32_t out_mas
         const nw_panel_proxy_ops ops{&px, RcclProxy::recv, RcclProxy::flag, RcclProxy::poison, RcclProxy::send};
         xrc = nw_panel_proxy_run(p->L1, p->xblk, p->prev >= 0, p->next >= 0, launched, &ops);
     }
-    if (launched) rc = nwi::fill_finish(t);
+    if (launched) {
+        rc = nwi::fill_finish(t);
+        if (rc != NW_OK) (void)post_credit(p, false, true);   // whatever the kernel got to
+    }
     if (p->transport == NW_PANEL_IPC && rc != NW_OK && p->next >= 0 && p->rows > 0 && p->L1 > 0) {
         // we owe the panel below a row we could not produce
         const int prc = nwi::poison(p->peer_xin[(size_t)p->next], p->L1, epoch, p->s_send);
@@ -534,6 +545,7 @@ int nw_panel_group_fill(nw_panel* const* ps, int n, int32_t m, int32_t k, int32_
         nw_panel* p = ps[r];
         if (stop) {
             rcs[(size_t)r] = NW_ERR_PEER;
+            (void)post_credit(p, false, true);
             continue;
         }
         if (p->rows > 0) {
@@ -542,10 +554,14 @@ int nw_panel_group_fill(nw_panel* const* ps, int n, int32_t m, int32_t k, int32_
             if (!launched[(size_t)r]) stop = true;
         }
         if (rcs[(size_t)r] == NW_OK) rcs[(size_t)r] = post_credit(p, launched[(size_t)r] && p->t->xin);
+        else (void)post_credit(p, false, true);
     }
     for (int r = 0; r < n; ++r) {
         nw_panel* p = ps[r];
-        if (launched[(size_t)r]) rcs[(size_t)r] = nwi::fill_finish(p->t);
+        if (launched[(size_t)r]) {
+            rcs[(size_t)r] = nwi::fill_finish(p->t);
+            if (rcs[(size_t)r] != NW_OK) (void)post_credit(p, false, true);
+        }
         if (rcs[(size_t)r] != NW_OK && p->next >= 0 && launched[(size_t)p->next] && p->L1 > 0) {
             nw_panel* q = ps[p->next];
             (void)hipSetDevice(q->device);
@@ -620,6 +636,8 @@ int nw_panel_hash_columns(nw_panel* p, uint64_t* hstate, uint64_t* dstate) {
     // the first panel hashes global row 0 (the seed) too; the others start at their first own row
     return nw_table_hash_columns(p->t, p->row_base == 0 ? 0 : 1, hstate, dstate);
 }
+
+int nw_panel_credit_reached(uint32_t credit, uint32_t want) { return nwk::epoch_reached(credit, want) ? 1 : 0; }
 
 int nw_panel_rows(const nw_panel* p, int64_t* row_base, int64_t* rows) {
     if (!p || !row_base || !rows) return fail(NW_ERR_ARG, "nw_panel_rows: bad arguments");

@@ -462,7 +462,7 @@ int nw_table_walk_elapsed_ms(nw_table* t, float* count_ms, float* path_ms) {
 }
 
 // ---------------------------------------------------------------------------
-// Banded checkpoint traceback (SURVEY.md 8(f) item 3): the first alignment the
+// Banded checkpoint traceback: the first alignment the
 // reference prints, for pairs whose full direction table does not fit.
 //
 //   1. Forward: the rows are cut into bands of `band_rows` (a multiple of 64).

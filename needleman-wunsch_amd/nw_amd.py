@@ -59,11 +59,13 @@ EXPORTS = (
     "nw_table_trace", "nw_table_count_alignments", "nw_table_first_path", "nw_table_walk_elapsed_ms",
     "nw_first_path_banded", "nw_table_hash_columns", "nw_hash_fold",
     "nw_host_alloc", "nw_host_free", "nw_table_io_stats", "nw_table_enumerate_paths",
+    "nw_table_layout", "nw_table_device_buffers",
     # include/nw_panel.h
     "nw_panel_partition", "nw_panel_chain", "nw_panel_get_id", "nw_panel_create", "nw_panel_ipc_handle",
     "nw_panel_ipc_connect", "nw_panel_group_create", "nw_panel_destroy", "nw_panel_set_sequences",
     "nw_panel_fill", "nw_panel_group_fill", "nw_panel_stats", "nw_panel_record", "nw_panel_reduce",
     "nw_panel_rows", "nw_panel_table", "nw_panel_elapsed_ms", "nw_panel_hash_columns", "nw_panel_proxy_run",
+    "nw_panel_credit_reached",
 )
 
 
@@ -73,9 +75,53 @@ class NWError(RuntimeError):
         self.rc = rc
 
 
+class Layout(ctypes.Structure):
+    """nw_layout (include/nw_fill.h): how the last fill laid the table out in HBM."""
+    _fields_ = [("score_pitch", ctypes.c_int64), ("NQ", ctypes.c_int64), ("pair", ctypes.c_int32),
+                ("skew", ctypes.c_int32), ("raw", ctypes.c_int32), ("SQ", ctypes.c_int32), ("SR", ctypes.c_int32),
+                ("d", ctypes.c_int32), ("has_scores", ctypes.c_int32), ("has_dirs", ctypes.c_int32)]
+
+
 class _Stats(ctypes.Structure):
     _fields_ = [("corner", ctypes.c_int32), ("greatest_abs_interior", ctypes.c_int32),
                 ("branch_count", ctypes.c_uint32)]
+
+
+def decode_tiles(tiles: np.ndarray, words: np.ndarray | None, L1: int, L2: int, d: int, lay=None):
+    """Dense (H, codes) from the device layout of include/nw_fill.h -- what a
+    zero-copy consumer computes.  tiles / words: the raw device buffers copied
+    to the host; lay: a Layout (None = the plain variant)."""
+    NQ = int(lay.NQ) if lay is not None else (L1 + 7) // 8
+    P = int(lay.score_pitch) if lay is not None else 512 * NQ
+    pair, skew, raw = (int(lay.pair), int(lay.skew), int(lay.raw)) if lay is not None else (0, 0, 0)
+    H = np.empty((L1 + 1, L2 + 1), dtype=np.int64)
+    H[:, 0] = -np.arange(L1 + 1, dtype=np.int64) * d
+    H[0, :] = -np.arange(L2 + 1, dtype=np.int64) * d
+    C = np.zeros((L1 + 1, L2 + 1), dtype=np.uint8)
+    C[1:, 0] = 4
+    C[0, 1:] = 2
+    if L1 and L2:
+        i = np.arange(1, L1 + 1, dtype=np.int64)[:, None]
+        j = np.arange(1, L2 + 1, dtype=np.int64)[None, :]
+        r, q = j - 1, i - 1
+        rr = 64 * (2 * (r // 128) + r % 2) + (r % 128) // 2 if pair else r
+        t = q + rr % 64 if skew else q
+        if tiles is not None:
+            x = tiles[(rr // 64) * P + ((t // 4) * 64 + rr % 64) * 4 + t % 4].astype(np.int64)
+            if raw:
+                SQ, SR = int(lay.SQ), int(lay.SR)
+                g = r // 128
+                big = SR * (SQ + 1)
+                s = np.where(g < big, g // (SQ + 1), SR + (g - big) // max(SQ, 1))
+                rw = r - 128 * (s * SQ + np.minimum(s, SR))
+                base = ((i - 1) // 4096) * 4096
+                x = x - (rw + i - base) * int(lay.d)
+            H[1:, 1:] = x
+        if words is not None:
+            w = words[((rr // 64) * (NQ + 1) + t // 8 + 1) * 64 + rr % 64].astype(np.int64)
+            C[1:, 1:] = ((w >> (21 - 3 * (t % 8))) & 7).astype(np.uint8)
+    H = ((H + 2**31) % 2**32 - 2**31).astype(np.int32)
+    return H, C
 
 
 @dataclass(frozen=True)
@@ -150,6 +196,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "nw_panel_table": (c_p, [c_p]),
         "nw_panel_elapsed_ms": (c_int, [c_p, P(ctypes.c_float), P(ctypes.c_float)]),
         "nw_panel_hash_columns": (c_int, [c_p, c_p, c_p]),
+        "nw_panel_credit_reached": (c_int, [c_u32, c_u32]),
         "nw_table_hash_columns": (c_int, [c_p, c_i64, c_p, c_p]),
         "nw_hash_fold": (ctypes.c_uint64, [c_p, c_i64]),
         "nw_table_count_alignments": (c_int, [c_p, P(c_u32)]),
@@ -161,6 +208,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "nw_table_enumerate_paths": (c_int, [c_p, ctypes.c_uint64, ctypes.c_uint64, c_p, c_i64, c_p,
                                              P(ctypes.c_uint64), P(ctypes.c_uint64)]),
         "nw_host_free": (None, [c_p]),
+        "nw_table_layout": (c_int, [c_p, P(Layout)]),
+        "nw_table_device_buffers": (c_int, [c_p, P(c_p), P(c_p)]),
         "nw_table_io_stats": (c_int, [c_p, P(ctypes.c_double), P(c_i64), P(ctypes.c_double), P(c_i64)]),
     }
     for name, (res, args) in sigs.items():
@@ -404,6 +453,19 @@ class Table:
     def waves(self) -> int:
         return self._lib.nw_table_waves(self._h)
 
+    def layout(self) -> Layout:
+        """Device layout of the last fill (nw_table_layout)."""
+        l = Layout()
+        _check(self._lib.nw_table_layout(self._h, ctypes.byref(l)), "nw_table_layout")
+        return l
+
+    def device_buffers(self) -> tuple[int, int]:
+        """Device addresses (score tiles, code words) for zero-copy consumers."""
+        a, b = ctypes.c_void_p(), ctypes.c_void_p()
+        _check(self._lib.nw_table_device_buffers(self._h, ctypes.byref(a), ctypes.byref(b)),
+               "nw_table_device_buffers")
+        return a.value or 0, b.value or 0
+
     @property
     def score_pitch(self) -> int:
         return self._lib.nw_table_score_pitch(self._h)
@@ -637,7 +699,7 @@ def first_path_banded(s1, s2, m: int, k: int, d: int, band_rows: int = 65536, de
 
 
 def gen_dna(seed: int, n: int) -> bytes:
-    """splitmix64 i.i.d. DNA (SURVEY.md 8(d)): base = "ACGT"[z >> 62]."""
+    """splitmix64 i.i.d. DNA: base = "ACGT"[z >> 62]."""
     if n == 0:
         return b""
     with np.errstate(over="ignore"):

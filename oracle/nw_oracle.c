@@ -16,7 +16,8 @@
  *
  * Arithmetic is 32-bit two's complement with wrap-around (the reference's
  * `int` arithmetic is undefined on overflow; parity is only claimed where no
- * intermediate overflows).
+ * intermediate overflows; the GPU library rejects such inputs with
+ * NW_ERR_RANGE).
  */
 #include "nw_oracle.h"
 

@@ -25,7 +25,7 @@ typedef struct {
         uint32_t branch_count;           /* interior cells with >=2 dirs    */
 } nwo_stats;
 
-/* splitmix64 DNA generator (SURVEY.md 8(d)): seed 1 -> s1, seed 2 -> s2. */
+/* splitmix64 DNA generator: seed 1 -> s1, seed 2 -> s2. */
 void nwo_gen_dna(uint64_t seed, int64_t n, char *out);
 
 /* FNV-1a-64 over a byte range, continuing from h. */

@@ -6,7 +6,7 @@ Writes tests/golden/big_scoreonly.json: the corner H[L1][L2] and the FNV-1a-64
 of the last column H[L1][0..L2] (int32 LE), from oracle/nw_oracle.c's
 nwo_score_only_mt (row bands on `threads` cores; equal to the serial
 nwo_score_only at every size tested, tests/test_oracle_golden.py).  Inputs:
-splitmix64 DNA seeds 1 and 2 (SURVEY.md 8(d)), m = k = d = 1.  The oracle is
+splitmix64 DNA seeds 1 and 2, m = k = d = 1.  The oracle is
 test infrastructure; this script only produces the fixture.
 """
 import json

@@ -192,7 +192,9 @@ def make_big():
         _fields_ = [("corner", ctypes.c_int32), ("gav", ctypes.c_int32), ("bc", ctypes.c_uint32)]
 
     out = []
-    for L1, L2, m, k, d in [(100000, 100000, 1, 1, 1)]:
+    # 100k x 100k (configs[2]) first: the tests index it as record 0; then
+    # configs[1] in the same column-chained form, for bench.py's C2 line.
+    for L1, L2, m, k, d in [(100000, 100000, 1, 1, 1), (10000, 10000, 1, 1, 1)]:
         b1, b2 = ctypes.create_string_buffer(L1), ctypes.create_string_buffer(L2)
         lib.nwo_gen_dna(ctypes.c_uint64(1), ctypes.c_int64(L1), b1)
         lib.nwo_gen_dna(ctypes.c_uint64(2), ctypes.c_int64(L2), b2)
@@ -300,7 +302,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true")
     ap.add_argument("--big-walk", action="store_true", help="only the 100k walk fixture (+ the fast ones)")
+    ap.add_argument("--only-big", action="store_true", help="rewrite big_colchain.json alone")
     a = ap.parse_args()
+    if a.only_big:
+        with open(os.path.join(HERE, "big_colchain.json"), "w") as f:
+            json.dump(make_big(), f, indent=1)
+        return
     if not os.path.exists(HARNESS):
         sys.exit("build the reference first: make -C oracle ref")
     with open(os.path.join(HERE, "ref_kats.json"), "w") as f:

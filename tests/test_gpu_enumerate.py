@@ -1,5 +1,4 @@
-"""Device-side enumeration of every optimal alignment (nw_table_enumerate_paths,
-SURVEY.md 8(f) item 4 -- the reference's parallel-traceback future work,
+"""Device-side enumeration of every optimal alignment (nw_table_enumerate_paths, the reference's parallel-traceback future work,
 README:195-200): each alignment is unranked on its own from the device's
 path-count table, and the sequence must be exactly the reference's print order
 (its depth-first walk, needleman-wunsch.c:209-331), restated over the oracle's

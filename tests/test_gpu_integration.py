@@ -1,4 +1,4 @@
-"""INTEGRATION.md's drop-in on the MI355X: the reference program itself
+"""The drop-in on the MI355X: the reference program itself
 (oracle/_ref/needleman-wunsch-gpu -- its own objects, compiled from its
 sources in the build container) with the call at needleman-wunsch.c:662
 served by integration/nw_gpu_shim.c -> nw_fill() -> libnwfill.so.  Every CLI

@@ -1,4 +1,4 @@
-"""Host I/O of the device-resident table (SURVEY.md 8(f) item 2): pinned
+"""Host I/O of the device-resident table: pinned
 sequence upload and streamed slice copies (nw_table_copy_scores /
 nw_table_copy_codes through two device staging buffers, DMA straight into
 pinned destinations or through pinned bounce buffers), checked against the

@@ -161,7 +161,7 @@ def test_ipc_two_processes(tmp_path, L1, L2, mkd):
 def test_ipc_back_to_back_delayed_consumer(tmp_path, delay_rank, world):
     """Back-to-back fills with different m, k, d while one consumer starts
     every fill 0.4 s late: the panels above run ahead into the next fill and
-    must wait for its credit (ADVICE r01: without back-pressure the producer
+    must wait for its credit (without back-pressure the producer
     overwrote a boundary row still being read, and the consumer timed out)."""
     L1, L2 = 3000, 1000
     seq = [(2, 3, 5), (1, 1, 1), (3, 1, 2), (1, 2, 1)]

@@ -101,7 +101,7 @@ def test_walk_arbitrary_bytes():
 def test_walk_empty_and_reuse():
     # empty strings: one path along the seeded row / column; none for two
     # empty strings -- the walk starts on (0,0), whose directions are all done
-    # (computation.c:96-99), so the reference counts 0 (ADVICE r01)
+    # (computation.c:96-99), so the reference counts 0
     for s1, s2 in [(b"", b"ACGT"), (b"ACGT", b""), (b"", b"")]:
         count, mv, _ = _walk(s1, s2, 1, 1, 1, max_L1=8, max_L2=8)
         assert count == (0 if not s1 and not s2 else 1)

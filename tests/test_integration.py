@@ -1,4 +1,4 @@
-"""INTEGRATION.md's drop-in, built for real (CPU side).
+"""The reference-side drop-in, built for real (CPU side).
 
 oracle/Makefile links the reference program from its own objects (compiled
 from /root/reference, never copied) with integration/nw_gpu_shim.c and

@@ -94,6 +94,20 @@ def test_reduce_semantics():
     assert rc == nw_amd.NW_ERR_PEER
 
 
+def test_credit_comparison_accepts_later_epochs_and_wraps():
+    """The producer's back-pressure wait (needleman-wunsch.c:444-452's wait on
+    the left neighbour, moved to one boundary row per panel) accepts the
+    awaited epoch or a later one: a consumer whose fill failed posts its
+    credit from the host, possibly for the epoch after the awaited one."""
+    reached = lambda c, w: bool(nw_amd.load().nw_panel_credit_reached(c, w))
+    assert reached(0, 0) and reached(5, 5) and reached(6, 5) and reached(1000, 5)
+    assert not reached(4, 5) and not reached(0, 1)
+    # epochs wrap from 2^31 - 1 to 1 (bit 31 is the poison bit)
+    top = 0x7FFFFFFF
+    assert reached(top, top) and reached(1, top) and reached(2, top - 1)
+    assert not reached(top - 1, top) and not reached(top, 1)
+
+
 def _band_fill(s1, s2, L2, n, r, top, m, k, d):
     base, rows = nw_amd.panel_partition(L2, n, r)
     return base, rows, O.fill_band(s1, s2[base:base + rows], base, top, m, k, d)
@@ -132,6 +146,25 @@ def _free_port():
         return s.getsockname()[1]
 
 
+class _OraclePanel:
+    """Stands in for a Panel on the CPU: continues the per-column FNV-1a-64
+    states over a band's own rows exactly as nw_panel_hash_columns does (the
+    first panel hashes global row 0 too, the others start at their first own
+    row)."""
+
+    def __init__(self, Hb, Db, first):
+        self.H, self.D, self.j0 = Hb, Db, 0 if first else 1
+
+    def hash_columns(self, state):
+        P = np.uint64(0x100000001B3)
+        with np.errstate(over="ignore"):
+            for j in range(self.j0, self.H.shape[1]):
+                x = self.H[:, j].astype(np.uint32).astype(np.uint64)
+                for b in range(4):
+                    state[0] = (state[0] ^ ((x >> np.uint64(8 * b)) & np.uint64(0xFF))) * P
+                state[1] = (state[1] ^ self.D[:, j].astype(np.uint64)) * P
+
+
 def _gloo_worker(rank, world, port, L1, L2, mkd, out_path):
     import torch
     import torch.distributed as dist
@@ -155,11 +188,17 @@ def _gloo_worker(rank, world, port, L1, L2, mkd, out_path):
     recs = bench_multi.gather_records(rec)
     slowest = bench_multi.max_over_ranks(float(rank + 1))
     tables = bench_multi.exchange_bytes(Hb[:, 1:].tobytes())
+    if rows and base == 0:
+        Db[0, 0], Db[1:, 0] = 0, 4                      # the band's row 0 is the table's seeded row 0
+    # every rank takes part, a rank without rows passes the states on untouched
+    hashes = bench_multi.chain_hash_states(_OraclePanel(Hb[:, :rows + 1 if rows else 0], Db, base == 0), L1, rank,
+                                           world)
     if rank == 0:
         rc, st = nw_amd.panel_reduce(recs)
         full = np.concatenate([np.frombuffer(t, dtype=np.int32).reshape(L1 + 1, -1) for t in tables], axis=1)
         np.savez(out_path, rc=rc, stats=np.array([st.corner, st.greatest_abs_interior, st.branch_count]),
-                 slowest=slowest, table=full, nrec=len(recs))
+                 slowest=slowest, table=full, nrec=len(recs),
+                 hashes=np.array(hashes if hashes else (0, 0), dtype=np.uint64))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -176,6 +215,9 @@ def test_gloo_two_ranks_chain(tmp_path, L1, L2):
     assert tuple(int(x) for x in z["stats"]) == st
     assert float(z["slowest"]) == 2.0
     np.testing.assert_array_equal(z["table"], H[:, 1:])
+    # the per-column hash states chained rank to rank fold to the whole table's hashes
+    h, e, _ = O.colchain(O.gen_dna(1, L1), O.gen_dna(2, L2), *mkd)
+    assert tuple(int(x) for x in z["hashes"]) == (h, e)
 
 
 # ------------------------------------------- RCCL host proxy (sequencing only)

@@ -54,6 +54,7 @@ RING2 = True
 # the chain against the issue count on the GPU (tools/ab_build_pair.sh).
 EXP_NO_BCAST = False
 EXP_NO_SCORES = False
+EXP_FLAGS9 = False     # 9 flag instructions per column instead of 12 (drops row b's three shift-ins)
 
 
 def GA(s):
@@ -147,6 +148,8 @@ def column_items(c, ST, HH=True, FF=True):
     its.append(It("bB2", "v_alignbit_b32 %[accB], %[accB], %[dUb], 31", ["Ub", "bB1"]))
     its.append(It("bA3", "v_alignbit_b32 %[accA], %[accA], %[dDa], 31", ["Da", "bA2"]))
     its.append(It("bB3", "v_alignbit_b32 %[accB], %[accB], %[dDb], 31", ["Db", "bB2"]))
+    if EXP_FLAGS9:
+        its = [it for it in its if it.name not in ("bB1", "bB2", "bB3")]
     if ST:
         its.append(It("Za", f"v_sub_u32_e32 %[tmp], 0, %[ha{c}]", ["Ha"]))
         its.append(It("Ma", f"v_max3_i32 %[gavA], %[gavA], %[ha{c}], %[tmp]", ["Za"]))
@@ -336,9 +339,11 @@ def main():
     ap.add_argument("--align", type=int, choices=(0, 4), default=ALIGN)
     ap.add_argument("--exp-no-bcast", action="store_true")
     ap.add_argument("--exp-no-scores", action="store_true")
+    ap.add_argument("--exp-flags9", action="store_true")
     args = ap.parse_args()
     globals()["EXP_NO_BCAST"] = args.exp_no_bcast
     globals()["EXP_NO_SCORES"] = args.exp_no_scores
+    globals()["EXP_FLAGS9"] = args.exp_flags9
     globals()["READ_AT"] = args.read_at
     globals()["ALIGN"] = args.align
     parts = ["// GENERATED by tools/gen_pair_asm.py -- do not edit; see the generator for the schedule.\n",

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Host I/O throughput of the device-resident table.
+"""Host I/O throughput of the device-resident table .
 
     python tools/io_bench.py > profiles/<round>_io_stream.json
 
