@@ -272,7 +272,9 @@ def cpu_baseline(n, threads, n_all=3000):
             T = max(2, min(threads, nproc))
             rp = run_ref(n, T)
             if rp is not None and "fill_s" in rp:
-                res["pthread"] = dict(_leg(n, rp, f"-p {T} (this GPU's CPU share of the host's {nproc})"), threads=T)
+                what = (f"-p {T} = -p $(nproc), configs[1]'s CPU leg" if T == nproc
+                        else f"-p {T} (this GPU's CPU share of the host's {nproc})")
+                res["pthread"] = dict(_leg(n, rp, what), threads=T)
             if nproc > T:
                 ra = run_ref(n_all, nproc, timeout=150)
                 if ra is not None and "fill_s" in ra:

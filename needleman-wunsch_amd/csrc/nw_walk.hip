@@ -584,6 +584,18 @@ int nw_table_enumerate_paths(nw_table* t, uint64_t first, uint64_t count, uint8_
             (void)hipFree(w->cnt);
             w->cnt = nullptr;
             w->cnt_bytes = 0;
+            // The path-count table is 8 bytes per cell, ~20x the direction
+            // codes: say so up front instead of failing inside hipMalloc
+            // ($NW_ENUM_MAX_BYTES caps it, e.g. to exercise a caller's fallback).
+            size_t free_b = 0, total_b = 0;
+            NW_HIPCHK(hipMemGetInfo(&free_b, &total_b));
+            if (const char* e = getenv("NW_ENUM_MAX_BYTES")) free_b = std::min<size_t>(free_b, (size_t)atoll(e));
+            if (need > free_b)
+                return nwi::fail(NW_ERR_OOM, "nw_table_enumerate_paths: the path-count table needs " +
+                                                 std::to_string(need) + " bytes (8 per cell), " +
+                                                 std::to_string(free_b) + " available on the device; copy the codes "
+                                                 "(nw_table_copy_codes) and walk them on the host, or use "
+                                                 "nw_table_first_path / nw_first_path_banded");
             NW_HIPCHK(hipMalloc(&w->cnt, need));
             w->cnt_bytes = need;
         }

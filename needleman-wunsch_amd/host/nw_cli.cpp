@@ -180,6 +180,34 @@ int main(int argc, char** argv) {
     PathBatches pb;
     pb.t = t;
     pb.stride = std::max<int64_t>(L1 + L2, 1);
+    if (listing) {
+        // The device enumeration keeps 8 bytes per cell.  When that does not
+        // fit, walk the codes on the host as the reference does
+        // (needleman-wunsch.c:209-331) -- slower, same output.
+        uint64_t total = 0;
+        const int prc = nw_table_enumerate_paths(t, 0, 0, nullptr, pb.stride, nullptr, nullptr, &total);
+        if (prc == NW_ERR_OOM) {
+            if (codes.empty()) {
+                codes.resize((size_t)((L1 + 1) * (L2 + 1)));
+                rc = nw_table_copy_codes(t, 0, L1 + 1, codes.data());
+                if (rc != NW_OK) {
+                    fprintf(stderr, "%s: error: GPU fill failed: %s: %s\n", g_prog, nw_strerror(rc), nw_last_error());
+                    exit(1);
+                }
+            }
+            if (nwh_render(s1, s2, &f, f.tflag ? H.data() : nullptr, codes.data(), st.corner,
+                           st.greatest_abs_interior, stdout, stderr) != 0) {
+                errno = ENOMEM;
+                log_err_errno("malloc failed");
+                exit(1);
+            }
+            nw_table_destroy(t);
+            free(s1);
+            free(s2);
+            if (in != stdin) fclose(in);
+            return 0;
+        }
+    }
     const int r = nwh_render_paths(s1, s2, &f, f.tflag ? H.data() : nullptr, f.tflag ? codes.data() : nullptr,
                                    st.corner, st.greatest_abs_interior, count, next_path, &pb, stdout, stderr);
     if (r == -2) {

@@ -231,34 +231,34 @@ def _check(rc: int, what: str) -> None:
 
 class HostBuffer:
     """Pinned (page-locked) host memory from nw_host_alloc, viewed as a numpy
-    array: slice copies into it are DMA'd straight from the device."""
+    array: slice copies into it are DMA'd straight from the device.
+
+    The memory belongs to the views: `array`, every slice or reshape of it and
+    every array a copy call returned for `out=hb.array` keep it alive, and it
+    goes back to the runtime when the last of them is gone.  close() only
+    drops this object's own view."""
 
     def __init__(self, shape, dtype):
+        import weakref
         lib = load()
         self.array_dtype = np.dtype(dtype)
         n = int(np.prod(shape)) * self.array_dtype.itemsize
-        self._p = ctypes.c_void_p()
-        _check(lib.nw_host_alloc(n, ctypes.byref(self._p)), "nw_host_alloc")
-        raw = (ctypes.c_uint8 * max(n, 1)).from_address(self._p.value)
+        p = ctypes.c_void_p()
+        _check(lib.nw_host_alloc(n, ctypes.byref(p)), "nw_host_alloc")
+        raw = (ctypes.c_uint8 * max(n, 1)).from_address(p.value)
+        # numpy keeps `raw` alive as the base of every view; the pinned
+        # memory is released when `raw` itself is collected
+        weakref.finalize(raw, lib.nw_host_free, ctypes.c_void_p(p.value))
         self.array = np.frombuffer(raw, dtype=np.uint8, count=n).view(self.array_dtype).reshape(shape)
 
     def close(self) -> None:
-        if self._p and self._p.value:
-            self.array = None
-            load().nw_host_free(self._p)
-            self._p = ctypes.c_void_p()
+        self.array = None
 
     def __enter__(self):
         return self
 
     def __exit__(self, *exc):
         self.close()
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
 
 
 def _bytes(s) -> bytes:

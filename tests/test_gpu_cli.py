@@ -16,6 +16,29 @@ def test_cli_matches_reference(case):
     assert run_cli(case) == (case["rc"], case["stdout"], case["stderr"])
 
 
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c["name"])
+def test_cli_host_walk_fallback_matches_reference(case, monkeypatch):
+    """When the device's path-count table (8 bytes per cell) does not fit, the
+    CLI walks the codes on the host (needleman-wunsch.c:209-331) instead of
+    failing; $NW_ENUM_MAX_BYTES = 0 forces that path for every golden."""
+    monkeypatch.setenv("NW_ENUM_MAX_BYTES", "0")
+    assert run_cli(case) == (case["rc"], case["stdout"], case["stderr"])
+
+
+def test_enumerate_paths_reports_missing_memory(monkeypatch):
+    import nw_amd
+    monkeypatch.setenv("NW_ENUM_MAX_BYTES", "1000")
+    with nw_amd.Table(300, 200) as t:
+        t.set_sequences(b"ACGT" * 75, b"TGCA" * 50)
+        t.fill(1, 1, 1, nw_amd.NW_OUT_ALL)
+        with pytest.raises(nw_amd.NWError) as e:
+            t.enumerate_paths(0, 1)
+        assert e.value.rc == nw_amd.NW_ERR_OOM and "8 per cell" in str(e.value)
+        monkeypatch.delenv("NW_ENUM_MAX_BYTES")
+        paths, total = t.enumerate_paths(0, 1)
+        assert len(paths) == 1 and total >= 1
+
+
 def test_cli_large_summary_and_quiet():
     """CLI on longer inputs.  -q alone skips the traceback (needleman-wunsch.c:667);
     -s runs it, so use a near-identical pair whose optimum is a single alignment

@@ -85,3 +85,21 @@ def test_megabase_upload_then_fill():
         lastcol = t.last_column()
         assert int(lastcol[-1]) == corner
         assert O.fnv(lastcol) == hlast
+
+
+def test_host_buffer_views_keep_the_pinned_memory_alive():
+    """An array taken out of a HostBuffer outlives it: the pinned memory is
+    released with the last view, not with the wrapper."""
+    import gc
+    a = nw_amd.HostBuffer((1 << 16,), np.int32).array      # the wrapper is gone at once
+    gc.collect()
+    a[:] = 7
+    hb = nw_amd.HostBuffer((4, 4), np.int32)
+    v = hb.array[1:]
+    hb.close()
+    gc.collect()
+    v[:] = 3
+    churn = [nw_amd.HostBuffer((1 << 16,), np.int32) for _ in range(8)]   # reuse of freed pinned pages would show
+    for c in churn:
+        c.array[:] = -1
+    assert int(a.sum()) == 7 << 16 and int(v.sum()) == 36
