@@ -263,6 +263,64 @@ int nw_first_path_banded(int device, const char *s1, int64_t L1, const char *s2,
 /* Device time (ms) of the last count / first-path kernel (HIP events). */
 int nw_table_walk_elapsed_ms(nw_table *t, float *count_ms, float *path_ms);
 
+/* ---------------------------------------------------------------------------
+ * nw_fill_noalloc: the fill for callers that cannot allocate -- code under
+ * HIP graph capture, tight serving loops, harnesses that forbid hipMalloc.
+ * It has no counterpart in the reference (whose tables are calloc'd per run,
+ * score-table.c:60-81); it is nw_table_fill() with every buffer either the
+ * caller's or a fixed array inside the library.
+ *
+ * It calls no hipMalloc / hipFree / hipHostMalloc nor any other allocating
+ * routine of the HIP runtime, on any path, and its success path does not
+ * touch the host heap either (only an error return builds a message for
+ * nw_last_error()).  It only enqueues work on `stream` (a hipStream_t, NULL
+ * = the null stream): one set-up kernel, the fill kernel, one result kernel.
+ * It does not wait for them; results are read from the caller's buffers
+ * after the caller has synchronised with `stream`.
+ *
+ * The caller passes, all in DEVICE memory of `device`:
+ *   s1_dev, s2_dev   the two sequences, L1 and L2 raw bytes (no padding)
+ *   score_tiles_dev  NW_NOALLOC_SCORE_ELEMS(L1, L2) int32, or NULL without
+ *                    NW_OUT_SCORES
+ *   dir_words_dev    NW_NOALLOC_DIR_WORDS(L1, L2) uint32, or NULL without
+ *                    NW_OUT_DIRS
+ *   last_column_dev  NULL or L2 + 1 int32: H[L1][0..L2]
+ *   result_dev       NULL or one nw_noalloc_result: status = 0 or the nw_err
+ *                    the kernel hit (NW_ERR_TIMEOUT), and the stats
+ *                    (greatest_abs_interior / branch_count only with
+ *                    NW_OUT_STATS, else 0)
+ * The tables come out in the device layout described above, always the
+ * plain variant: pair = skew = raw = 0, P = 512 * ceil(L1/8).
+ *
+ * Everything else the fill needs (padded copies of the sequences, control
+ * words, the score-only last-column staging, the hand-off rows between
+ * workgroup stripes) is in one static device array of
+ * NW_NOALLOC_SCRATCH_BYTES inside the library, which each GPU the library
+ * runs on holds until the process ends; its size is what limits L1 and L2
+ * to NW_NOALLOC_MAX_L1 / NW_NOALLOC_MAX_L2 -- beyond them the call returns
+ * NW_ERR_ARG and enqueues nothing (use nw_table_fill).  All calls on one GPU
+ * share that array: two calls whose work overlaps on one GPU (different
+ * streams, or threads) race; calls on one stream, or otherwise ordered, are
+ * fine, and each call clears what it needs at zero itself.
+ * Returns 0 once the work is enqueued, or a negative nw_err (arguments,
+ * NW_ERR_RANGE, a failed launch).
+ */
+#define NW_NOALLOC_MAX_L1 16384
+#define NW_NOALLOC_MAX_L2 16384
+#define NW_NOALLOC_SCRATCH_BYTES (9 * 1024 * 1024)
+#define NW_NOALLOC_SCORE_ELEMS(L1, L2) \
+        ((((int64_t)(L2) + 63) / 64 + 1) * (((int64_t)(L1) + 7) / 8 + 8) * 512)
+#define NW_NOALLOC_DIR_WORDS(L1, L2) \
+        ((((int64_t)(L2) + 63) / 64 + 1) * (((int64_t)(L1) + 7) / 8 + 9) * 64)
+typedef struct nw_noalloc_result {
+        int32_t  status;
+        nw_stats stats;
+} nw_noalloc_result;
+int nw_fill_noalloc(int device, void *stream, const char *s1_dev, int64_t L1, const char *s2_dev,
+                    int64_t L2, int32_t m, int32_t k, int32_t d, uint32_t out_mask,
+                    int32_t *score_tiles_dev, uint32_t *dir_words_dev, int32_t *last_column_dev,
+                    nw_noalloc_result *result_dev);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1502,3 +1502,196 @@ int nw_fill(const char* s1, int64_t L1, const char* s2, int64_t L2, int32_t m, i
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ no-alloc
+// nw_fill_noalloc (include/nw_fill.h): the fill for callers that cannot
+// allocate.  Everything the fill kernel needs beyond the caller's inputs and
+// outputs -- the padded copies of the two sequences, the control words, the
+// last-column staging of a score-only fill and the WG-stripe hand-off
+// granules -- lives in one file-scope device array, `scratch`.  Every GPU the
+// library runs on holds its own copy of the array at its own address; host
+// code only ever uses the address hipGetSymbolAddress returned for that GPU
+// (na_state.ptr), never the array's name.
+namespace {
+
+constexpr int64_t kNaMaxL1 = NW_NOALLOC_MAX_L1, kNaMaxL2 = NW_NOALLOC_MAX_L2;
+constexpr int64_t kNaNC = (kNaMaxL1 + CH - 1) / CH, kNaNG = (kNaMaxL2 + 63) / 64;
+constexpr int kNaW = 4;                                       // stripes per workgroup
+constexpr int64_t kNaSlots = (kNaNG + kNaW - 1) / kNaW + 1;   // one per WG-stripe + 1
+constexpr size_t na_align(size_t x) { return (x + 255) & ~(size_t)255; }
+constexpr size_t kNaCtl = 0;                                              // CTL_WORDS uint32
+constexpr size_t kNaS1 = na_align(kNaCtl + CTL_WORDS * 4);                // CH*NC + 64 bytes
+constexpr size_t kNaS2 = na_align(kNaS1 + (size_t)(CH * kNaNC + 64));     // 64*NG + 1024 bytes
+constexpr size_t kNaLast = na_align(kNaS2 + (size_t)(64 * kNaNG + 1024)); // (64*NG + 128) int32
+constexpr size_t kNaGran = na_align(kNaLast + (size_t)(64 * kNaNG + 128) * 4);
+constexpr size_t kNaBytes = na_align(kNaGran + (size_t)(kNaSlots * (CH * kNaNC + CH)) * 8);
+static_assert(kNaBytes <= NW_NOALLOC_SCRATCH_BYTES, "scratch layout exceeds its stated size");
+
+static __device__ __align__(256) unsigned char scratch[NW_NOALLOC_SCRATCH_BYTES];
+
+struct NaState {
+    unsigned char* ptr = nullptr;   // this device's copy of `scratch` (hipGetSymbolAddress)
+    int ncu = 0;
+    int rc = NW_OK;
+    bool ready = false;
+};
+constexpr int kNaMaxDev = 64;
+NaState g_na[kNaMaxDev];
+std::atomic_flag g_na_lock = ATOMIC_FLAG_INIT;
+
+// Once per device, with that device current.
+const NaState& na_state(int device) {
+    while (g_na_lock.test_and_set(std::memory_order_acquire)) {
+    }
+    NaState& st = g_na[device];
+    if (!st.ready) {
+        st.ready = true;
+        hipDeviceProp_t prop;
+        void* p = nullptr;
+        hipError_t e = hipGetDeviceProperties(&prop, device);
+        if (e == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            st.rc = fail(NW_ERR_NODEVICE, std::string("nw_fill_noalloc: device is ") + prop.gcnArchName +
+                                              ", this library is built for gfx950 only");
+        } else {
+            if (e == hipSuccess) e = hipGetSymbolAddress(&p, HIP_SYMBOL(scratch));
+            if (e != hipSuccess || !p)
+                st.rc = fail(NW_ERR_HIP, std::string("nw_fill_noalloc: hipGetSymbolAddress(scratch): ") +
+                                             hipGetErrorString(e));
+            else {
+                st.ptr = static_cast<unsigned char*>(p);
+                st.ncu = prop.multiProcessorCount;
+            }
+        }
+    }
+    g_na_lock.clear(std::memory_order_release);
+    return st;
+}
+
+// Padded copies of the sequences (the fill kernel reads whole chunks and whole
+// stripes), the control words and the granule slots this fill uses start at
+// zero.  A kernel, not hipMemsetAsync: the call may be recorded into a graph.
+__global__ void nw_na_prep_kernel(unsigned char* sc, const char* s1, int32_t L1, const char* s2, int32_t L2,
+                                  int64_t n1, int64_t n2, int64_t ngran) {
+    const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, nth = (int64_t)gridDim.x * blockDim.x;
+    if (tid < CTL_WORDS) reinterpret_cast<uint32_t*>(sc + kNaCtl)[tid] = 0u;
+    for (int64_t x = tid; x < n1; x += nth) sc[kNaS1 + x] = x < L1 ? (unsigned char)s1[x] : 0;
+    for (int64_t x = tid; x < n2; x += nth) sc[kNaS2 + x] = x < L2 ? (unsigned char)s2[x] : 0;
+    uint64_t* g = reinterpret_cast<uint64_t*>(sc + kNaGran);
+    for (int64_t x = tid; x < ngran; x += nth) g[x] = 0ull;
+}
+
+// Results: status + stats, and the last column H[L1][0..L2].
+__global__ void nw_na_finish_kernel(const unsigned char* sc, TableView v, int32_t L1, int32_t L2, int32_t d, int sh,
+                                    int stt, int32_t* last, nw_noalloc_result* res) {
+    const uint32_t* ctl = reinterpret_cast<const uint32_t*>(sc + kNaCtl);
+    const int32_t* lc = reinterpret_cast<const int32_t*>(sc + kNaLast);
+    auto cell = [&](int64_t j) -> int32_t {
+        if (L1 == 0 || j == 0) return (int32_t)(-(L1 + j) * (int64_t)d);
+        return sh ? score_at(v, L1, j) : lc[j];
+    };
+    const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, nth = (int64_t)gridDim.x * blockDim.x;
+    if (last)
+        for (int64_t j = tid; j <= L2; j += nth) last[j] = cell(j);
+    if (tid == 0 && res) {
+        res->status = (int32_t)ctl[CTL_ERR];
+        res->stats.corner = cell(L2);
+        res->stats.greatest_abs_interior = stt ? (int32_t)ctl[CTL_GAV] : 0;
+        res->stats.branch_count = stt ? ctl[CTL_BC] : 0u;
+    }
+}
+
+}  // namespace
+
+extern "C" int nw_fill_noalloc(int device, void* stream, const char* s1_dev, int64_t L1, const char* s2_dev,
+                               int64_t L2, int32_t m, int32_t k, int32_t d, uint32_t out_mask,
+                               int32_t* score_tiles_dev, uint32_t* dir_words_dev, int32_t* last_column_dev,
+                               nw_noalloc_result* result_dev) {
+    if (L1 < 0 || L2 < 0 || (L1 && !s1_dev) || (L2 && !s2_dev) || device < 0 || device >= kNaMaxDev)
+        return fail(NW_ERR_ARG, "nw_fill_noalloc: bad arguments");
+    if (L1 > kNaMaxL1 || L2 > kNaMaxL2)
+        return fail(NW_ERR_ARG, "nw_fill_noalloc: " + std::to_string(L1) + " x " + std::to_string(L2) +
+                                    " is beyond the scratch array's limit of " + std::to_string(kNaMaxL1) + " x " +
+                                    std::to_string(kNaMaxL2) + " (use nw_table_fill)");
+    if (((out_mask & NW_OUT_SCORES) && !score_tiles_dev) || ((out_mask & NW_OUT_DIRS) && !dir_words_dev))
+        return fail(NW_ERR_ARG, "nw_fill_noalloc: an output in out_mask has no buffer");
+    {
+        const int64_t M = std::max({std::llabs(m), std::llabs(k), std::llabs(d)});
+        const int64_t bound = (L1 + L2) * M + 6144 * std::llabs(d) + 4 * M + 2;   // as nwi::fill_launch
+        if (bound >= (int64_t)INT32_MAX)
+            return fail(NW_ERR_RANGE, "nw_fill_noalloc: |scores| could reach " + std::to_string(bound));
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev)
+        return fail(NW_ERR_NODEVICE, "nw_fill_noalloc: device ordinal out of range");
+    int cur = 0;
+    HIPCHK(hipGetDevice(&cur));
+    if (cur != device) HIPCHK(hipSetDevice(device));
+    struct Restore {
+        int cur, device;
+        ~Restore() {
+            if (cur != device) (void)hipSetDevice(cur);
+        }
+    } restore{cur, device};
+    const NaState& st = na_state(device);
+    if (st.rc != NW_OK) return st.rc;
+    unsigned char* const sc = st.ptr;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const bool sh = out_mask & NW_OUT_SCORES, sd = out_mask & NW_OUT_DIRS, stt = out_mask & NW_OUT_STATS;
+    const int64_t NC = (L1 + CH - 1) / CH, NG = (L2 + 63) / 64;
+    TableView v{};
+    v.tiles = score_tiles_dev;
+    v.spitch = 512 * NC;
+    v.D = sd ? dir_words_dev : nullptr;
+    v.NC = (int32_t)NC;
+    v.d = d;
+    if (L1 > 0 && L2 > 0) {
+        // WG-stripes of up to 4 stripes, dealt evenly (every SIMD its own
+        // compute wave), taken in order from the dequeue: any grid completes.
+        const int W = (int)std::min<int64_t>(kNaW, NG);
+        const int64_t NSW = (NG + W - 1) / W;
+        KernelFn fn = pick_kernel(W, false, sh, sd, stt);
+        if (!fn) return fail(NW_ERR_ARG, "nw_fill_noalloc: unsupported wave count");
+        const int64_t grid = std::min<int64_t>(NSW, (int64_t)st.ncu * 2);
+        FillArgs a{};
+        a.s1 = sc + kNaS1;
+        a.s2 = sc + kNaS2;
+        a.L1 = (int32_t)L1;
+        a.L2 = (int32_t)L2;
+        a.m = m;
+        a.k = k;
+        a.d = d;
+        a.NC = a.NCH = (int32_t)NC;
+        a.NG = (int32_t)NG;
+        a.NSW = (int32_t)NSW;
+        a.SQ = (int32_t)(NG / NSW);
+        a.SR = (int32_t)(NG % NSW);
+        a.H = score_tiles_dev;
+        a.spitch = 512 * NC;
+        a.D = dir_words_dev;
+        a.lastcol = reinterpret_cast<int32_t*>(sc + kNaLast);
+        a.gran = reinterpret_cast<uint64_t*>(sc + kNaGran);
+        a.gpitch = CH * NC + CH;
+        a.nslot = (int32_t)(grid + 1);
+        a.ctl = reinterpret_cast<uint32_t*>(sc + kNaCtl);
+        a.spin_ticks = SPIN_TICKS;
+        a.xblk = 1;
+        a.gtag = 1u << 16;
+        const int64_t ngran = NSW > 1 ? (int64_t)a.nslot * a.gpitch : 0;
+        if ((size_t)ngran * 8 > kNaBytes - kNaGran) return fail(NW_ERR_ARG, "nw_fill_noalloc: granule scratch too small");
+        nw_na_prep_kernel<<<256, 256, 0, s>>>(sc, s1_dev, (int32_t)L1, s2_dev, (int32_t)L2, CH * NC + 64,
+                                              64 * NG + 1024, ngran);
+        HIPCHK(hipGetLastError());
+        void* kargs[] = {&a};
+        HIPCHK(hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3((unsigned)grid), dim3(64 * (W + 2)), kargs, 0, s));
+        HIPCHK(hipGetLastError());
+    } else {
+        nw_na_prep_kernel<<<1, 64, 0, s>>>(sc, s1_dev, 0, s2_dev, 0, 0, 0, 0);   // the control words only
+        HIPCHK(hipGetLastError());
+    }
+    if (last_column_dev || result_dev) {
+        nw_na_finish_kernel<<<64, 256, 0, s>>>(sc, v, (int32_t)L1, (int32_t)L2, d, sh ? 1 : 0, stt ? 1 : 0,
+                                               last_column_dev, result_dev);
+        HIPCHK(hipGetLastError());
+    }
+    return NW_OK;
+}

@@ -59,7 +59,7 @@ EXPORTS = (
     "nw_table_trace", "nw_table_count_alignments", "nw_table_first_path", "nw_table_walk_elapsed_ms",
     "nw_first_path_banded", "nw_table_hash_columns", "nw_hash_fold",
     "nw_host_alloc", "nw_host_free", "nw_table_io_stats", "nw_table_enumerate_paths",
-    "nw_table_layout", "nw_table_device_buffers",
+    "nw_table_layout", "nw_table_device_buffers", "nw_fill_noalloc",
     # include/nw_panel.h
     "nw_panel_partition", "nw_panel_chain", "nw_panel_get_id", "nw_panel_create", "nw_panel_ipc_handle",
     "nw_panel_ipc_connect", "nw_panel_group_create", "nw_panel_destroy", "nw_panel_set_sequences",
@@ -85,6 +85,35 @@ class Layout(ctypes.Structure):
 class _Stats(ctypes.Structure):
     _fields_ = [("corner", ctypes.c_int32), ("greatest_abs_interior", ctypes.c_int32),
                 ("branch_count", ctypes.c_uint32)]
+
+
+class NoallocResult(ctypes.Structure):
+    """nw_noalloc_result (include/nw_fill.h)."""
+    _fields_ = [("status", ctypes.c_int32), ("stats", _Stats)]
+
+
+NW_NOALLOC_MAX_L1 = 16384
+NW_NOALLOC_MAX_L2 = 16384
+
+
+def noalloc_score_elems(L1: int, L2: int) -> int:
+    """NW_NOALLOC_SCORE_ELEMS: int32 elements of the caller's score-tile buffer."""
+    return ((L2 + 63) // 64 + 1) * ((L1 + 7) // 8 + 8) * 512
+
+
+def noalloc_dir_words(L1: int, L2: int) -> int:
+    """NW_NOALLOC_DIR_WORDS: uint32 words of the caller's code-word buffer."""
+    return ((L2 + 63) // 64 + 1) * ((L1 + 7) // 8 + 9) * 64
+
+
+def fill_noalloc(device: int, stream, s1_dev: int, L1: int, s2_dev: int, L2: int, m: int, k: int, d: int,
+                 out_mask: int, score_tiles_dev: int = 0, dir_words_dev: int = 0, last_column_dev: int = 0,
+                 result_dev: int = 0) -> int:
+    """nw_fill_noalloc on raw device addresses; returns the status code (the
+    work is only enqueued on `stream`)."""
+    return load().nw_fill_noalloc(device, stream, s1_dev or None, L1, s2_dev or None, L2, m, k, d, out_mask,
+                                  score_tiles_dev or None, dir_words_dev or None, last_column_dev or None,
+                                  result_dev or None)
 
 
 def decode_tiles(tiles: np.ndarray, words: np.ndarray | None, L1: int, L2: int, d: int, lay=None):
@@ -208,6 +237,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "nw_table_enumerate_paths": (c_int, [c_p, ctypes.c_uint64, ctypes.c_uint64, c_p, c_i64, c_p,
                                              P(ctypes.c_uint64), P(ctypes.c_uint64)]),
         "nw_host_free": (None, [c_p]),
+        "nw_fill_noalloc": (c_int, [c_int, c_p, c_p, c_i64, c_p, c_i64, c_i32, c_i32, c_i32, c_u32, c_p, c_p, c_p, c_p]),
         "nw_table_layout": (c_int, [c_p, P(Layout)]),
         "nw_table_device_buffers": (c_int, [c_p, P(c_p), P(c_p)]),
         "nw_table_io_stats": (c_int, [c_p, P(ctypes.c_double), P(c_i64), P(ctypes.c_double), P(c_i64)]),
