@@ -51,7 +51,7 @@ SHIFT_INTO_T = True
 RING2 = True
 # Timing-only experiments (wrong results; never the product): drop the two
 # cross-row prefix levels (row_bcast:15/31) and/or the score adds, to price
-# the chain against the issue count on the GPU (tools/ab_build_pair.sh).
+# the chain against the issue count on the GPU (GEN=... PAIR_ONLY=1 tools/ab_build.sh).
 EXP_NO_BCAST = False
 EXP_NO_SCORES = False
 EXP_FLAGS9 = False     # 9 flag instructions per column instead of 12 (drops row b's three shift-ins)

@@ -20,7 +20,7 @@ B=(bench.py --L1 "$L1" --L2 "$L2" --no-cpu-baseline --no-c2)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
     python3 "${B[@]}" --steps 20 --warmup 5 > "$OUT/kt.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/wr" -o run -- \
-    python3 "${B[@]}" --steps 2 --warmup 0 > "$OUT/wr.log" 2>&1
+    python3 "${B[@]}" --no-hash --steps 2 --warmup 0 > "$OUT/wr.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/rd" -o run -- \
-    python3 "${B[@]}" --steps 2 --warmup 0 > "$OUT/rd.log" 2>&1
+    python3 "${B[@]}" --no-hash --steps 2 --warmup 0 > "$OUT/rd.log" 2>&1
 python3 tools/pmc_traffic.py "$RND" "$OUT" "$L1" "$L2" 5
