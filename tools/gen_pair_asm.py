@@ -192,10 +192,18 @@ def block(ST, P, HH=True, FF=True):
            # (READ_AT: how late in the block the next slot is read; the
            # producer runs one chunk ahead, so an early read usually misses it
            # and the caller takes the slow re-read)
-           READ_AT: [It("PQ", "ds_read_b64 %[pq], %[cb] offset:8", lds=True),       # {prog[w], cons[w+1]}
-                     It("TA", "ds_read_b128 %[nA], %[rd]", lds=True)],
-           READ_AT + 1: [It("TB", "ds_read_b128 %[nB], %[rd] offset:16", lds=True),
-                         It("TC", "ds_read_b64 %[nC], %[rd] offset:32", lds=True)]}
+           }
+    reads = [It("PQ", "ds_read_b64 %[pq], %[cb] offset:8", lds=True),       # {prog[w], cons[w+1]}
+             It("TA", "ds_read_b128 %[nA], %[rd]", lds=True),
+             It("TB", "ds_read_b128 %[nB], %[rd] offset:16", lds=True),
+             It("TC", "ds_read_b64 %[nC], %[rd] offset:32", lds=True)]
+    # READ_AT <= 6: two reads in that step's gaps, two in the next step's;
+    # 7: all four in step 7's; 8: all four in the tail (after column 7's shift)
+    if READ_AT <= 6:
+        mem.setdefault(READ_AT, []).extend(reads[:2])
+        mem.setdefault(READ_AT + 1, []).extend(reads[2:])
+    elif READ_AT == 7:
+        mem.setdefault(7, []).extend(reads)
     # head: profile lookups of the chunk, pre-fill of sh_1
     if P:
         out += [It("", "v_perm_b32 %[subA0], %[pha], %[pla], %[tc0]"),
@@ -239,6 +247,8 @@ def block(ST, P, HH=True, FF=True):
     # tail: D and F of column 7, its codes / scores / ring write, then prog
     done.discard("F")
     pool = column_items(7, ST, HH, FF)
+    if READ_AT >= 8:
+        pool = reads + pool
     gap(pool)
     emit(It("D", f"v_mov_b32_dpp %[{SH(8)}], %[{GB(7)}] wave_shr:1 row_mask:0xf bank_mask:0xf"))
     emit(It("F", f"v_max_i32_e32 %[{GA(7)}], %[{XA(7)}], %[{SH(8)}]"))
