@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build an A/B variant of libnwfill.so into lib_ab/ from the current sources:
-#   [GEN="gen_pair_asm.py flags"] [PAIR_ONLY=1] bash tools/ab_build.sh NAME [hipcc flags, e.g. -DNW_TRACE_EXT=1]
+#   [GEN="gen_pair_asm.py flags"] [GEN_SCAN="gen_chunk_asm.py flags"] [PAIR_ONLY=1] bash tools/ab_build.sh NAME [hipcc flags, e.g. -DNW_TRACE_EXT=1]
 # GEN regenerates the pair kernel's block (tools/gen_pair_asm.py, e.g.
 # "--exp-no-bcast", "--align 0") into the variant's private copy of csrc/.
 # PAIR_ONLY=1 recompiles only nw_pair.hip and links the in-tree objects of the
@@ -14,6 +14,9 @@ W=$(mktemp -d)
 cp -r "$ROOT/needleman-wunsch_amd/csrc" "$W/csrc"
 if [ -n "${GEN:-}" ]; then
   python3 "$ROOT/tools/gen_pair_asm.py" --out "$W/csrc/nw_pair_chunk.inc" $GEN > /dev/null
+fi
+if [ -n "${GEN_SCAN:-}" ]; then   # the one-row scan kernel's block (tools/gen_chunk_asm.py)
+  python3 "$ROOT/tools/gen_chunk_asm.py" --out "$W/csrc/nw_chunk.inc" $GEN_SCAN > /dev/null
 fi
 mkdir -p "$ROOT/lib_ab"
 HIPFLAGS=(--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -Xclang -target-feature -Xclang -packed-fp32-ops -I"$ROOT/include")

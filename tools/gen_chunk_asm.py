@@ -60,6 +60,7 @@ STORE = "normal"       # score stores: normal | fixed (diagnostic: one address)
 STORE_HINT = "nt"      # cache-policy bits of the score stores (e.g. "nt", "sc1")
 SCORE_X4 = True        # scores leave as 2 x global_store_dwordx4 per chunk from C++ (quad tiles)
 CODE_HINT = "nt"       # cache-policy bits of the code-word stores
+EXP_NO_BCAST = False   # timing-only experiment (wrong results): drop the two cross-row prefix levels
 
 
 def gname(s):
@@ -219,6 +220,8 @@ def step(s, N, F, H, A, S, SD, nxt, floating, P=False):
     ]
     dpps = ["row_shr:1 row_mask:0xf", "row_shr:2 row_mask:0xf", "row_shr:4 row_mask:0xf",
             "row_shr:8 row_mask:0xf", "row_bcast:15 row_mask:0xa", "row_bcast:31 row_mask:0xc"]
+    if EXP_NO_BCAST:
+        dpps = dpps[:4]
     out = []
     done = set()
     pending = list(fill)
@@ -360,7 +363,7 @@ def tf(b):
 
 
 def main():
-    global OUT, READ_STEP, STORE, STORE_HINT, SCORE_X4, CODE_HINT
+    global OUT, READ_STEP, STORE, STORE_HINT, SCORE_X4, CODE_HINT, EXP_NO_BCAST
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=OUT)
     ap.add_argument("--read-step", type=int, default=READ_STEP)
@@ -368,7 +371,9 @@ def main():
     ap.add_argument("--store-hint", default=STORE_HINT)
     ap.add_argument("--x4", type=int, default=int(SCORE_X4))
     ap.add_argument("--code-hint", default=CODE_HINT)
+    ap.add_argument("--exp-no-bcast", action="store_true")
     args = ap.parse_args()
+    EXP_NO_BCAST = args.exp_no_bcast
     OUT, READ_STEP, STORE, STORE_HINT = args.out, args.read_step, args.store, args.store_hint
     SCORE_X4 = bool(args.x4)
     CODE_HINT = args.code_hint
