@@ -92,12 +92,14 @@ int nw_fill(const char *s1, int64_t L1, const char *s2, int64_t L2,
  *
  * Device layout (for zero-copy consumers; everyone else uses the copy, hash
  * and walk entry points below, which decode it).  Which variant a fill left
- * in the table is reported by nw_table_layout(); the three fill kernels
- * (column scan, skewed stripes, two rows per lane -- chosen per shape, or by
- * $NW_KERNEL) share the tiling and differ in how a cell's row r = j - 1 and
- * column q = i - 1 map into it:
+ * in the table is reported by nw_table_layout(); the four fill kernels
+ * (column scan, skewed stripes, two rows per lane, skewed 16-row groups --
+ * chosen per shape, or by $NW_KERNEL) share the tiling and differ in how a
+ * cell's row r = j - 1 and column q = i - 1 map into it:
  *   rr = pair ? 64*(2*(r/128) + r%2) + (r%128)/2 : r     (two rows per lane)
- *   t  = skew ? q + rr%64 : q                            (stored by step)
+ *   t  = skew == 1 ? q + rr%64                           (stored by step)
+ *      : skew == 2 ? q + (rr%64)/16                      (16-row groups one step apart)
+ *      : q
  *   scores: stripe quad tiles.  Row 0 and column 0 (the seeds -i*d, -j*d) are
  *           not stored.  Interior cell (i, j) is element
  *             (rr/64)*P + ((t/4)*64 + rr%64)*4 + t%4,
@@ -119,7 +121,10 @@ int nw_fill(const char *s1, int64_t L1, const char *s2, int64_t L2,
  *             rw = r - 128*(s*SQ + min(s, SR));  base = ((i-1)/4096)*4096
  *             H  = G' - (rw + i - base)*d
  *           with SQ, SR, d from nw_layout (the fill's stripe plan and indel
- *           penalty).  Every entry point below returns H, never G'.
+ *           penalty).  A fill with NW_OUT_SCORES that the 16-row-group kernel
+ *           ran (nw_layout.raw = 2) does the same with 64-row stripes and no
+ *           moving base: g = r/64, rw = r - 64*(s*SQ + min(s, SR)), base = 0,
+ *           H = G' - (rw + i)*d.  Every entry point below returns H, never G'.
  */
 typedef struct nw_table nw_table;
 
@@ -187,8 +192,8 @@ typedef struct nw_layout {
         int64_t score_pitch;   /* P: int32 elements per 64-row stripe           */
         int64_t NQ;            /* 8-column groups per stripe                     */
         int32_t pair;          /* rows permuted (two-rows-per-lane kernel)       */
-        int32_t skew;          /* stored by step (skewed-stripe kernel)          */
-        int32_t raw;           /* score tiles hold G', see "raw scores"          */
+        int32_t skew;          /* stored by step: 1 skewed stripes, 2 16-row groups */
+        int32_t raw;           /* score tiles hold G' (1 | 2), see "raw scores"   */
         int32_t SQ, SR;        /* raw: the fill's workgroup-stripe plan          */
         int32_t d;             /* raw: the fill's indel penalty                  */
         int32_t has_scores, has_dirs;

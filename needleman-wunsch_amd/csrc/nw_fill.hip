@@ -909,7 +909,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
     NW_HIPCHK(hipEventRecord(t->ev[0], t->stream));
     NW_HIPCHK(hipMemsetAsync(t->ctl, 0, CTL_WORDS * 4, t->stream));
     int W = 0;
-    bool skew = false, pair = false;
+    bool skew = false, pair = false, quad = false, autosel = false;
     int32_t pSQ = 0, pSR = 0;
     if (L1 > 0 && L2 > 0) {
         StripePlan plan = plan_stripes(t->NG, t->ncu, 12);
@@ -927,11 +927,12 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
         // ~1.2 us per stripe, so the skew kernel wins only on very wide tables
         // with few stripes (measured: 1M x 20k 61 vs 75 ms, 100k x 64 4.6 vs
         // 6.2 ms; 100k x 12.5k 8.0 vs 7.0 ms and 100k x 100k 22 vs 11 ms the
-        // other way).  $NW_KERNEL = scan | skew | pair | auto (default).
+        // other way).  $NW_KERNEL = scan | skew | pair | quad | auto (default).
         const char* ke = getenv("NW_KERNEL");
         if (ke && std::strcmp(ke, "skew") == 0) skew = true;
         else if (ke && std::strcmp(ke, "scan") == 0) skew = false;
         else if (ke && std::strcmp(ke, "pair") == 0) pair = true;
+        else if (ke && std::strcmp(ke, "quad") == 0) quad = true;
         else {
             // auto (profiles/r01_ab_skew_vs_scan_shapes.txt,
             // r01_ab_kernels_after_publisher.txt, r01_ab_pair_scoreonly.txt):
@@ -942,16 +943,30 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
             // (skew from L1 >= 32*L2: it won at 100k x 64 and 1M x 20k, lost
             // at 100k x 12.5k -- an 8-GPU row panel -- 8.03 vs 7.04 ms,
             // profiles/r02_ab_loader.txt)
+            // (quad instead of scan wherever the fill needs no stats:
+            // 100k x 12.5k 6.46 -> 5.92 ms, 100k x 50k 7.23 -> 6.92 ms, 10k^2
+            // equal, profiles/r03m_ab_quad.txt)
             const int64_t simds = 4 * (int64_t)t->ncu;
             pair = t->NG > simds;
             skew = !pair && t->NG <= simds && L1 >= 32 * L2;
+            autosel = true;
         }
         // a feeding panel's last row must be lane 63's row b of its last pair stripe
         if (pair && t->xout && L2 % 128 != 0) pair = false;
+        if (autosel && !pair && !skew) quad = true;
+        // The quad kernel (nw_quad.hip) has no stats variant and works in
+        // G' = H + r*d + i*d without a moving column base: fall back to the
+        // scan kernel where that could leave int32.
+        if (quad) {
+            const int64_t M = std::max({std::llabs(m), std::llabs(k), std::llabs(d)});
+            const int64_t L2g = t->L2_total >= 0 ? t->L2_total : t->L2;
+            if (stt || (t->L1 + L2g) * M + (L1 + 2048) * std::llabs(d) + 4 * M + 2 >= (int64_t)INT32_MAX) quad = false;
+        }
         if (!skew && !pair) {
             plan = plan_stripes(t->NG, t->ncu, 12, 8, true);
             W = plan.W;
         }
+        if (quad && !pick_quad(W, prof, sh, sd)) quad = false;   // (a wave count it is not built for)
         const int64_t NGk = pair ? (L2 + 127) / 128 : t->NG;
         if (pair) {
             // Dequeued WG-stripes (more than 15 pair stripes per CU): 12 high
@@ -963,9 +978,11 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
             W = plan.W;
         }
         KernelFn fn = skew ? pick_skew(W, prof, sh, sd, stt)
-                           : pair ? pick_pair(W, prof, sh, sd, stt) : pick_kernel(W, prof, sh, sd, stt);
+                           : pair ? pick_pair(W, prof, sh, sd, stt)
+                                  : quad ? pick_quad(W, prof, sh, sd) : pick_kernel(W, prof, sh, sd, stt);
         if (!fn) return fail(NW_ERR_ARG, "nw_table_fill: unsupported wave count");
-        const int64_t NCH = skew ? (L1 + 63 + CH - 1) / CH : t->NC;
+        // chunks of 8 steps per stripe (quad: row group q runs q columns behind)
+        const int64_t NCH = skew ? (L1 + 63 + CH - 1) / CH : quad ? (L1 + 3 + CH - 1) / CH : t->NC;
         t->spitch = 512 * NCH;          // per 64-row stripe (a pair stripe is two of them)
         FillArgs a{};
         a.s1 = t->s1;
@@ -1021,7 +1038,7 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
             a.trace = t->trace + 8;
         }
         int occ = 1;
-        const int wgw = W + (skew ? 1 : 2);   // + loader (+ publisher: scan and pair kernels)
+        const int wgw = W + (skew ? 1 : 2);   // + loader (+ publisher: scan, pair and quad kernels)
         NW_HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(fn), 64 * wgw, 0));
         occ = std::max(occ, 1);
         // A panel leaves room on every CU for the kernels of its neighbours
@@ -1061,10 +1078,10 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
     t->pend_mask = out_mask;
     t->pend_d = d;
     t->pend_W = W;
-    t->pend_skew = skew;
+    t->pend_skew = skew ? 1 : quad ? 2 : 0;
     t->pend_pair = pair;
     // the pair kernel's fills with scores and without stats store G' (RAW in nw_pair.hip)
-    t->pend_raw = pair && sh && !stt;
+    t->pend_raw = (pair && sh && !stt) ? 1 : (quad && sh) ? 2 : 0;
     t->pend_SQ = pSQ;
     t->pend_SR = pSR;
     return NW_OK;
@@ -1095,7 +1112,7 @@ int fill_finish(nw_table* t) {
     }
     NW_HIPCHK(hipStreamSynchronize(t->stream));
     if (L1 > 0 && L2 > 0 && sh && t->pend_raw)
-        corner = (int32_t)((uint32_t)corner - raw_offset(L1, L2, t->pend_SQ, t->pend_SR, d));
+        corner = (int32_t)((uint32_t)corner - raw_offset(L1, L2, t->pend_SQ, t->pend_SR, d, t->pend_raw));
     if (ctl[CTL_ERR])
         return fail((int)ctl[CTL_ERR], (int)ctl[CTL_ERR] == NW_ERR_PEER
                                            ? "nw_table_fill: the panel above failed"

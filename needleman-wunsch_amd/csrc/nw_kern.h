@@ -192,9 +192,9 @@ struct TableView {
     int64_t spitch;
     const uint32_t* D;      // codes, or null
     int32_t NC;             // chunks per stripe of the layout (scan: ceil(L1/8); skew: ceil((L1+63)/8))
-    int32_t skew;           // 1: skewed layout (nw_skew.hip), 0: column layout (scan kernel)
+    int32_t skew;           // 0: column layout; 1: skewed by lane (nw_skew.hip); 2: by 16-lane row (nw_quad.hip)
     int32_t pair;           // 1: column layout with rows permuted (nw_pair.hip)
-    int32_t raw;            // 1: the tiles hold the pair kernel's G' (see raw_offset)
+    int32_t raw;            // 1: the tiles hold the pair kernel's G', 2: the quad kernel's (see raw_offset)
     int32_t SQ, SR;         // raw: the fill's WG-stripe plan (FillArgs)
     int32_t d;
     int32_t row_base;       // panels: global row of local row 0
@@ -209,14 +209,20 @@ struct TableView {
 // column i = 4q + r + 1 at g*spitch + (q*64 + l)*4 + r, so a lane's 4
 // consecutive columns are one 16-byte store and a chunk is 2 KB contiguous.
 // Column tiles: g*spitch + (i-1)*64 + l, one 256-byte store per column.
-// Skewed layout (nw_skew.inc): stored by step t = c + (r & 63) instead of
-// by column, same quad tiles.
+// Skewed layouts: stored by step instead of by column, same quad tiles.
+// skew = 1 (nw_skew.hip): step t = c + (r & 63), every lane one column behind
+// the lane above; skew = 2 (nw_quad.hip): t = c + ((r & 63) >> 4), every
+// 16-lane DPP row one column behind the row above.
 // Pair layout (nw_pair.hip): the column layout of the permuted row
 // nwi::pair_row(r).
-__host__ __device__ __forceinline__ int64_t score_index(int64_t r, int64_t c, int64_t spitch, bool skew = false,
+__host__ __device__ __forceinline__ int64_t skew_off(int skew, int64_t lane) {
+    return skew == 1 ? lane : skew == 2 ? lane >> 4 : 0;
+}
+
+__host__ __device__ __forceinline__ int64_t score_index(int64_t r, int64_t c, int64_t spitch, int skew = 0,
                                                          bool pair = false) {
     if (pair) r = nwi::pair_row(r);
-    if (skew) c += r & 63;
+    c += skew_off(skew, r & 63);
 #if NW_SCORE_X4
     return (r >> 6) * spitch + ((c >> 2) * 64 + (r & 63)) * 4 + (c & 3);
 #else
@@ -225,11 +231,11 @@ __host__ __device__ __forceinline__ int64_t score_index(int64_t r, int64_t c, in
 }
 
 // Code word and bit position of interior cell (i, j) (see include/nw_fill.h).
-__host__ __device__ __forceinline__ int64_t code_word(int64_t i, int64_t j, int64_t NC, bool skew, int* shift,
+__host__ __device__ __forceinline__ int64_t code_word(int64_t i, int64_t j, int64_t NC, int skew, int* shift,
                                                       bool pair = false) {
     const int64_t rr = pair ? nwi::pair_row(j - 1) : j - 1;
     const int64_t g = rr >> 6, l = rr & 63;
-    const int64_t t = (i - 1) + (skew ? l : 0);
+    const int64_t t = (i - 1) + skew_off(skew, l);
     *shift = 21 - 3 * (int)(t & 7);
     return (g * (NC + 1) + (t >> 3) + 1) * 64 + l;
 }
@@ -239,13 +245,15 @@ __host__ __device__ __forceinline__ int64_t code_word(int64_t i, int64_t j, int6
 // g0 = s*SQ + min(s, SR) .. of WG-stripe s, 128 rows each), base = the first
 // column of the cell's 4096-column super-chunk.  H = G' - raw_offset (mod 2^32,
 // as the kernel computes).
-__host__ __device__ __forceinline__ uint32_t raw_offset(int64_t i, int64_t j, int SQ, int SR, int32_t d) {
-    const int64_t rr = j - 1, g = rr >> 7;
+// The quad kernel (raw = 2) has 64-row stripes and no column base: G' = H + r*d + i*d.
+__host__ __device__ __forceinline__ uint32_t raw_offset(int64_t i, int64_t j, int SQ, int SR, int32_t d, int raw = 1) {
+    const int sh = raw == 2 ? 6 : 7;
+    const int64_t rr = j - 1, g = rr >> sh;
     const int64_t big = (int64_t)SR * (SQ + 1);
     const int64_t s = g < big ? g / (SQ + 1) : SR + (g - big) / SQ;
     const int64_t g0 = s * SQ + (s < SR ? s : SR);
-    const int64_t r = rr - 128 * g0;
-    const int64_t base = ((i - 1) >> 12) << 12;
+    const int64_t r = rr - (g0 << sh);
+    const int64_t base = raw == 2 ? 0 : ((i - 1) >> 12) << 12;
     return (uint32_t)(r + (i - base)) * (uint32_t)d;
 }
 
@@ -253,7 +261,7 @@ __device__ __forceinline__ int32_t score_at(const TableView& v, int64_t i, int64
     if (i == 0) return (int32_t)(-(j + v.row_base) * (int64_t)v.d);
     if (j == 0) return v.top ? v.top[i - 1] + v.d : (int32_t)(-i * (int64_t)v.d);
     const int32_t x = v.tiles[score_index(j - 1, i - 1, v.spitch, v.skew, v.pair)];
-    return v.raw ? (int32_t)((uint32_t)x - raw_offset(i, j, v.SQ, v.SR, v.d)) : x;
+    return v.raw ? (int32_t)((uint32_t)x - raw_offset(i, j, v.SQ, v.SR, v.d, v.raw)) : x;
 }
 
 // Direction code of cell (i, j).  A panel's row 0 belongs to the panel above
@@ -277,5 +285,7 @@ using KernelFn = void (*)(FillArgs);
 KernelFn pick_skew(int W, bool prof, bool sh, bool sd, bool stt);
 // nw_pair.hip: the two-rows-per-lane scan kernel.
 KernelFn pick_pair(int W, bool prof, bool sh, bool sd, bool stt);
+// nw_quad.hip: the one-row scan kernel with 16-lane skewed row groups (no stats).
+KernelFn pick_quad(int W, bool prof, bool sh, bool sd);
 
 }  // namespace nwk

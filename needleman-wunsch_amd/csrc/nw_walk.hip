@@ -91,7 +91,7 @@ __global__ __launch_bounds__(64) void nw_count_kernel(CountArgs a) {
         uint32_t P = 1;         // column 0: (0,j) has only the up code, P = 1
         uint32_t Tprev = 1;     // P(0, 64g)
         // this lane's step of column i is t = i - 1 (+ lane in the skewed layout)
-        const int toff = a.skew ? lane : 0;
+        const int toff = (int)nwk::skew_off(a.skew, lane);
         uint32_t w = 0, wn = a.NC > 0 ? Dg[(int64_t)(toff >> 3) * 64] : 0u;
         bool dead = false;
         for (int i0 = 1; i0 <= a.L1 && !dead; i0 += CBLK) {
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(64) void nw_first_path_kernel(const uint32_t* D, in
     int64_t qb = -1;
     while (i > 0 && j > 0) {
         const int g = (j - 1) >> 6;
-        const int64_t t = (i - 1) + (skew ? ((j - 1) & 63) : 0);   // step of (i, j) in its stripe
+        const int64_t t = (i - 1) + nwk::skew_off(skew, (j - 1) & 63);   // step of (i, j) in its stripe
         const int64_t q = t >> 3, q0 = q & ~(int64_t)7;
         if (g != gb || q0 != qb) {
             __syncthreads();

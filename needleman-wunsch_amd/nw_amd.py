@@ -134,16 +134,17 @@ def decode_tiles(tiles: np.ndarray, words: np.ndarray | None, L1: int, L2: int, 
         j = np.arange(1, L2 + 1, dtype=np.int64)[None, :]
         r, q = j - 1, i - 1
         rr = 64 * (2 * (r // 128) + r % 2) + (r % 128) // 2 if pair else r
-        t = q + rr % 64 if skew else q
+        t = q + rr % 64 if skew == 1 else q + (rr % 64) // 16 if skew == 2 else q
         if tiles is not None:
             x = tiles[(rr // 64) * P + ((t // 4) * 64 + rr % 64) * 4 + t % 4].astype(np.int64)
             if raw:
                 SQ, SR = int(lay.SQ), int(lay.SR)
-                g = r // 128
+                hgt = 64 if raw == 2 else 128            # rows per stripe of the kernel that wrote them
+                g = r // hgt
                 big = SR * (SQ + 1)
                 s = np.where(g < big, g // (SQ + 1), SR + (g - big) // max(SQ, 1))
-                rw = r - 128 * (s * SQ + np.minimum(s, SR))
-                base = ((i - 1) // 4096) * 4096
+                rw = r - hgt * (s * SQ + np.minimum(s, SR))
+                base = 0 if raw == 2 else ((i - 1) // 4096) * 4096
                 x = x - (rw + i - base) * int(lay.d)
             H[1:, 1:] = x
         if words is not None:

@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 SD = nw_amd.NW_OUT_SCORES | nw_amd.NW_OUT_DIRS
 
 
-@pytest.fixture(params=["scan", "skew", "pair"])
+@pytest.fixture(params=["scan", "skew", "pair", "quad"])
 def fill_kernel(request, monkeypatch):
     monkeypatch.setenv("NW_KERNEL", request.param)
     monkeypatch.delenv("NW_WAVES", raising=False)
@@ -115,6 +115,23 @@ def test_sd_arbitrary_bytes_and_ties(fill_kernel):
     _check_sd(b"ACGT" * 300, b"TGCA" * 200, 1, 2, 1)
 
 
+@pytest.mark.parametrize("mask", [nw_amd.NW_OUT_SCORES, nw_amd.NW_OUT_DIRS, 0])
+@pytest.mark.parametrize("L1,L2", [(3, 70), (8, 64), (21, 200), (1000, 777), (5001, 64 * 9 + 1)])
+def test_partial_masks_vs_oracle(fill_kernel, mask, L1, L2):
+    """Scores only, codes only, score-only (last column): each its own kernel variant."""
+    s1, s2 = O.gen_dna(41, L1), O.gen_dna(42, L2)
+    Ho, Do, sto = O.fill(s1, s2, 2, 3, 5)
+    with nw_amd.Table(L1, L2, SD) as t:
+        t.set_sequences(s1, s2)
+        t.fill(2, 3, 5, mask)
+        assert t.stats().corner == sto[0]
+        assert np.array_equal(t.last_column(), Ho[-1])
+        if mask & nw_amd.NW_OUT_SCORES:
+            assert np.array_equal(t.scores(), Ho)
+        if mask & nw_amd.NW_OUT_DIRS:
+            assert np.array_equal(t.codes(), Do)
+
+
 def test_sd_refill_and_mask_changes(pair_kernel):
     """Raw and plain fills alternate on one table: each reader follows the
     last fill's encoding."""
@@ -148,7 +165,7 @@ def test_sd_10k_config_c2(auto_kernel, ref_kats):
     assert "%016x" % O.fnv(D) == case["hD"]
 
 
-@pytest.mark.parametrize("kernel", ["auto", "pair", "scan"])
+@pytest.mark.parametrize("kernel", ["auto", "pair", "scan", "quad"])
 def test_sd_100k_config_c3_hashes(monkeypatch, kernel):
     """configs[2] exactly as bench.py times it (scores + codes, no stats): the
     45 GB table hashes, on the device, to the fixture's whole-table hashes."""
@@ -182,7 +199,9 @@ def test_header_layout_formulas_decode_the_device_buffers(fill_kernel, L1, L2, m
         t.fill(*mkd, mask)
         lay = t.layout()
         assert lay.has_scores and lay.has_dirs
-        assert lay.raw == (1 if fill_kernel == "pair" and not (mask & nw_amd.NW_OUT_STATS) else 0)
+        stats = bool(mask & nw_amd.NW_OUT_STATS)       # (the quad kernel has no stats variant: the scan kernel runs)
+        assert lay.raw == (0 if stats else {"pair": 1, "quad": 2}.get(fill_kernel, 0))
+        assert lay.skew == (1 if fill_kernel == "skew" else 2 if fill_kernel == "quad" and not stats else 0)
         assert lay.score_pitch == t.score_pitch
         hp, dp = t.device_buffers()
         NG, NC = (L2 + 63) // 64, (L1 + 7) // 8

@@ -17,10 +17,12 @@ import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
 
-@pytest.fixture(params=["scan", "skew", "pair"], autouse=True)
+@pytest.fixture(params=["scan", "skew", "pair", "quad"], autouse=True)
 def fill_kernel(request, monkeypatch):
     """Every test runs on every fill kernel (nw_fill.hip's column scan,
-    nw_skew.hip's skewed stripes, nw_pair.hip's two-row scan), whose device layouts differ."""
+    nw_skew.hip's skewed stripes, nw_pair.hip's two-row scan, nw_quad.hip's
+    skewed 16-row groups; a fill with stats that asks for the last runs the
+    first), whose device layouts differ."""
     monkeypatch.setenv("NW_KERNEL", request.param)
     return request.param
 

@@ -15,13 +15,20 @@ cp -r "$ROOT/needleman-wunsch_amd/csrc" "$W/csrc"
 if [ -n "${GEN:-}" ]; then
   python3 "$ROOT/tools/gen_pair_asm.py" --out "$W/csrc/nw_pair_chunk.inc" $GEN > /dev/null
 fi
+if [ -n "${GEN_QUAD:-}" ]; then   # the quad kernel's block (tools/gen_quad_asm.py)
+  python3 "$ROOT/tools/gen_quad_asm.py" --out "$W/csrc/nw_quad_chunk.inc" $GEN_QUAD > /dev/null
+fi
 if [ -n "${GEN_SCAN:-}" ]; then   # the one-row scan kernel's block (tools/gen_chunk_asm.py)
   python3 "$ROOT/tools/gen_chunk_asm.py" --out "$W/csrc/nw_chunk.inc" $GEN_SCAN > /dev/null
 fi
 mkdir -p "$ROOT/lib_ab"
 HIPFLAGS=(--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -Xclang -target-feature -Xclang -packed-fp32-ops -I"$ROOT/include")
 OBJS=()
-for f in nw_fill nw_skew nw_pair nw_panel nw_walk; do
+for f in nw_fill nw_skew nw_pair nw_quad nw_panel nw_walk; do
+  if [ -n "${ONLY:-}" ] && [ "$f" != "$ONLY" ]; then
+    OBJS+=("$OBJ/$f.o")
+    continue
+  fi
   if [ -n "${PAIR_ONLY:-}" ] && [ "$f" != nw_pair ]; then
     OBJS+=("$OBJ/$f.o")
     continue
