@@ -34,6 +34,10 @@
 
 #include "nw_kern.h"
 
+#ifndef NW_PAIR_PIPE
+#define NW_PAIR_PIPE 1     // 0: the raw scores + codes fill runs the unpipelined block (pair_chunk_raw)
+#endif
+
 namespace nwk {
 namespace {
 
@@ -75,6 +79,13 @@ struct PairRegs {
     int gavA, gavB;     // in/out: running max |H| (stats)
     uint64_t pq;        // out: {prog[w], cons[w+1]} read mid-chunk
     int nloa, nlob;     // H = G' + nlo - (s+1)d (moved by -8d per chunk by the caller)
+    // pair_chunk_pipe (raw scores + codes, pipelined across blocks): G' of
+    // columns 4..7 of rows a / b in fixed registers (.w = the carried ga / gb),
+    // column 7's diagonal candidates, and accA / accB = the block's code words
+    // still without column 7 (flags inverted); the next block -- or
+    // flush_pending -- finishes and stores them.
+    v4i qa1, qb1;
+    int dga1, dgb1;
 };
 struct PairConst {
     int kd[8];          // -(s+1)*d
@@ -110,6 +121,8 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
     // itself, the readers add the affine offset back (nwk::raw_offset; the
     // table's raw flag).  Two v_add3 fewer per column: 100k^2 9.21 -> 8.89 ms.
     constexpr bool RAW = SH && !ST;
+    // (raw scores + codes: the block pipelined across chunks, pair_chunk_pipe)
+    constexpr bool PIPE = RAW && SD && NW_PAIR_PIPE;
     constexpr int NOCONS = 1 << 30;
     __shared__ __attribute__((aligned(16))) int tring[(W + 1) * R * SLOT];
     __shared__ __attribute__((aligned(8))) int ctr[2 * W + 4];
@@ -394,8 +407,37 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                 a.trace[8 * (int64_t)sidx + 4] = __builtin_amdgcn_s_memtime();
             }
             if (a.trace && lane == 0 && w == nw - 1) a.trace[8 * (int64_t)sidx + 6] = __builtin_amdgcn_s_memrealtime();
+            // ---- the pipelined block's state (PIPE): `pend` = the chunk whose
+            // column-7 flags, code words and scores of columns 4..7 are still
+            // in registers (-1: none) ----
+            r.qa1 = r.qb1 = v4i{0, 0, 0, 0};
+            r.dga1 = r.dgb1 = 0;
+            r.accA = r.accB = 0;
+            int pend = -1;
+            // byte offsets of this lane from the SGPR bases of the block's stores
+            int voa = lane * 16, vob = voa + (int)((tileB - tileA) * 4);
+            int vda = lane * 4, vdb = vda + (int)((dtileB - dtileA) * 4);
+            asm volatile("" : "+v"(voa), "+v"(vob), "+v"(vda), "+v"(vdb));
+            auto flush_pending = [&]() {
+                if (PIPE && pend >= 0) {
+                    auto lt = [](int x, int y) { return ((uint32_t)x - (uint32_t)y) >> 31; };   // 1: x < y (a flag not set)
+                    const int ga6 = r.qa1[2], ga7 = r.qa1[3], gb6 = r.qb1[2], gb7 = r.qb1[3];
+                    const uint32_t accA =
+                        ((r.accA << 3) | (lt(ga6, ga7) << 2) | (lt(r.sh, ga7) << 1) | lt(r.dga1, ga7)) ^ 0xffffffu;
+                    const uint32_t accB =
+                        ((r.accB << 3) | (lt(gb6, gb7) << 2) | (lt(ga7, gb7) << 1) | lt(r.dgb1, gb7)) ^ 0xffffffu;
+                    __builtin_nontemporal_store(r.qa1, reinterpret_cast<v4i*>(tileA + (int64_t)pend * 512 + 256 + lane * 4));
+                    __builtin_nontemporal_store(r.qb1, reinterpret_cast<v4i*>(tileB + (int64_t)pend * 512 + 256 + lane * 4));
+                    __builtin_nontemporal_store(accA, dtileA + (int64_t)(pend + 1) * 64 + lane);
+                    __builtin_nontemporal_store(accB, dtileB + (int64_t)(pend + 1) * 64 + lane);
+                    r.ga = ga7;
+                    r.gb = gb7;
+                    pend = -1;
+                }
+            };
             auto rebase = [&](int c) {
                 if (c > 0 && c % SUPER_CHUNKS == 0) {
+                    flush_pending();
                     const int shv = SUPER_CHUNKS * CH * d;
                     r.ga -= shv;
                     r.gb -= shv;
@@ -495,9 +537,30 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                     __builtin_amdgcn_s_sleep(1);
                 }
             };
-            auto full_chunk = [&](int c, auto slotc, PairSlot& cur, PairSlot& nxt) -> bool {
+            auto full_chunk = [&](int c, auto slotc, PairSlot& cur, PairSlot& nxt, bool head = false) -> bool {
                 constexpr int Q = decltype(slotc)::value;
-                if constexpr (RAW) {
+                if constexpr (PIPE) {
+                    // The block stores the pending chunk's second half and code
+                    // words (the chunk before this one) and its own scores of
+                    // columns 0..3.  With nothing pending those stores carry
+                    // stale registers: they go to this chunk's own second half
+                    // (rewritten by the next block or the flush, later in this
+                    // wave's program order) and to the code tiles' padding row.
+                    // (only a run's head chunk can have nothing pending)
+                    const bool fresh = head && pend < 0;
+                    const int32_t* hbs = tileA + (int64_t)c * 512;
+                    const int32_t* hbp = fresh ? hbs : hbs - 512;
+                    const uint32_t* dbp = fresh ? dtileA : dtileA + (int64_t)c * 64;
+                    if (fresh) {
+                        r.qa1[3] = r.ga;
+                        r.qb1[3] = r.gb;
+                    }
+                    pair_chunk_pipe<PROF>(r, kc, cur, nxt, c + 1, ra[Q], rd[(Q + 1) % R], voa, vob, vda, vdb, hbs, hbp, dbp);
+                    pend = c;
+                    if (c + 2 >= NC) return true;
+                    if (uni((int)(uint32_t)r.pq) > c + 1 && uni((int)(r.pq >> 32)) >= c + 2 - R) return true;
+                    return wait_slot(c + 1, nxt);
+                } else if constexpr (RAW) {
                     pair_chunk_raw<SD, PROF>(r, kc, cur, nxt, c + 1, ra[Q], rd[(Q + 1) % R]);
                     r.ha[7] = r.ga;
                     r.hb[7] = r.gb;
@@ -536,18 +599,19 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                 // [8*NSW + g]: when this stripe reaches the middle of the table
                 if (NW_TRACE_EXT && a.trace && lane == 0 && c == trace_mid_chunk(NC, R))
                     *trace_ext(a, TX_MID, g) = __builtin_amdgcn_s_memrealtime();
-                aborted = !full_chunk(c, S0{}, tA, tB) || !full_chunk(c + 1, S1{}, tB, tA) ||
+                aborted = !full_chunk(c, S0{}, tA, tB, true) || !full_chunk(c + 1, S1{}, tB, tA) ||
                           !full_chunk(c + 2, S2{}, tA, tB) || !full_chunk(c + 3, S3{}, tB, tA);
                 c += R;
             }
             if (!aborted && c < nfull) {
                 rebase(c);
-                aborted = !full_chunk(c, S0{}, tA, tB);
+                aborted = !full_chunk(c, S0{}, tA, tB, true);
                 if (!aborted && c + 1 < nfull) aborted = !full_chunk(c + 1, S1{}, tB, tA);
                 if (!aborted && c + 2 < nfull) aborted = !full_chunk(c + 2, S2{}, tA, tB);
                 c = nfull;
             }
             if (!aborted) {
+                flush_pending();
                 rebase(c);
                 aborted = !generic_chunk(c);
             }

@@ -26,6 +26,19 @@ and the chunk's LDS traffic (cons, the next slot's {prog, cons}, 8 T and the
 chunk's symbols, the symbols down the ring, prog after the last ring write).
 The block ends with lgkmcnt(K), K = the LDS ops issued after its last read.
 
+pair_chunk_pipe<P> (raw scores + codes, the 100k x 100k fill) is software
+pipelined across blocks: column 7's twelve flag instructions, the code words'
+final xor and every table store would otherwise run after the block, outside
+any DPP gap, while step 0's gaps (no previous column in this block) sit
+empty.  So a block leaves column 7's candidates in carried registers and the
+NEXT block finishes the previous block's code words in its step-0..3 gaps and
+stores them together with the previous block's scores of columns 4..7; its
+own scores of columns 0..3 go out in the gaps of steps 4..7.  The G'
+registers of a row are fixed VGPRs (v80..v87 row a, v88..v95 row b) so that
+four columns are one global_store_dwordx4 from inside the block; addresses
+are an SGPR base plus a per-lane VGPR offset.  The caller flushes the last
+block's pending half (nw_pair.hip).
+
 Template pair_chunk_asm<HH, FF, ST, P>: HH = scores, FF = direction codes
 (score-only fills skip both), ST = |H| max for the stats (rows a, b apart;
 needs HH and FF), P = profile lookups (symbols coded 0..7) instead of byte
@@ -55,6 +68,10 @@ RING2 = True
 EXP_NO_BCAST = False
 EXP_NO_SCORES = False
 EXP_FLAGS9 = False     # 9 flag instructions per column instead of 12 (drops row b's three shift-ins)
+# pair_chunk_pipe: the fixed VGPRs of G' (row a columns 0..7, row b columns 0..7)
+PIPE_REGS = {**{f"ga{s}": f"v{80 + s}" for s in range(7)}, "gac": "v87",
+             **{f"gb{s}": f"v{88 + s}" for s in range(7)}, "gbc": "v95"}
+PIPE_DEADLINE = 3      # step by whose end the previous block's deferred work is out
 
 
 def GA(s):
@@ -88,8 +105,34 @@ def T(s):
 
 
 class It:
-    def __init__(self, name, text, deps=(), lds=False):
-        self.name, self.text, self.deps, self.lds = name, text, list(deps), lds
+    def __init__(self, name, text, deps=(), lds=False, carry=False):
+        self.name, self.text, self.deps, self.lds, self.carry = name, text, list(deps), lds, carry
+
+
+def deferred_items():
+    """pair_chunk_pipe, step 0: the previous block's column-7 flags (its G' of
+    columns 6, 7 are still in the fixed registers, its dg and shift in carried
+    operands), code words and stores of columns 4..7."""
+    C = dict(carry=True)
+    its = [It("pLb", "v_sub_u32_e32 %[pLb], %[gb6], %[gbc]", **C),
+           It("pDb", "v_sub_u32_e32 %[pDb], %[pdgb], %[gbc]", **C),
+           It("pUb", "v_sub_u32_e32 %[pUb], %[gac], %[gbc]", **C),
+           It("pLa", "v_sub_u32_e32 %[pLa], %[ga6], %[gac]", **C),
+           It("pUa", "v_sub_u32_e32 %[pUa], %[shc], %[gac]", **C),
+           It("pDa", "v_sub_u32_e32 %[pDa], %[pdga], %[gac]", **C),
+           It("sQb1", "global_store_dwordx4 %[vob], v[92:95], %[hbp] offset:1024 nt", **C),
+           It("sQa1", "global_store_dwordx4 %[voa], v[84:87], %[hbp] offset:1024 nt", **C),
+           It("qA1", "v_alignbit_b32 %[tA], %[pA], %[pLa], 31", ["pLa"], **C),
+           It("qB1", "v_alignbit_b32 %[tB], %[pB], %[pLb], 31", ["pLb"], **C),
+           It("qA2", "v_alignbit_b32 %[tA], %[tA], %[pUa], 31", ["pUa", "qA1"], **C),
+           It("qB2", "v_alignbit_b32 %[tB], %[tB], %[pUb], 31", ["pUb", "qB1"], **C),
+           It("qA3", "v_alignbit_b32 %[tA], %[tA], %[pDa], 31", ["pDa", "qA2"], **C),
+           It("qB3", "v_alignbit_b32 %[tB], %[tB], %[pDb], 31", ["pDb", "qB2"], **C),
+           It("xA", "v_xor_b32_e32 %[tA], 0xffffff, %[tA]", ["qA3"], **C),
+           It("xB", "v_xor_b32_e32 %[tB], 0xffffff, %[tB]", ["qB3"], **C),
+           It("stA", "global_store_dword %[vda], %[tA], %[dbp] nt", ["xA"], **C),
+           It("stB", "global_store_dword %[vdb], %[tB], %[dbp] nt", ["xB"], **C)]
+    return its
 
 
 def sub_items(s, P, row):
@@ -158,9 +201,10 @@ def column_items(c, ST, HH=True, FF=True):
     return its
 
 
-def block(ST, P, HH=True, FF=True):
+def block(ST, P, HH=True, FF=True, pipe=False):
     out = []          # list of It
     done = set()
+    carried = []      # pipe: items that may move on into the next step's gaps
 
     def emit(it):
         out.append(it)
@@ -218,6 +262,15 @@ def block(ST, P, HH=True, FF=True):
         if not SHIFT_INTO_T or s == 7:
             pool.append(It("P", f"v_mov_b32_e32 %[{SH(s + 1)}], %[{T(s)}]"))        # lane 0's next shift
         pool += mem.get(s, [])
+        if pipe:
+            if s == 0:
+                carried = deferred_items()
+            if s == 4:
+                # this block's scores of columns 0..3: row b is final after step
+                # 3's scan, row a after step 4's F
+                carried += [It("sQb0", "global_store_dwordx4 %[vob], v[88:91], %[hbs] nt", carry=True),
+                            It("sQa0", "global_store_dwordx4 %[voa], v[80:83], %[hbs] nt", ["F"], carry=True)]
+            pool += carried
         chain = []
         if s > 0:
             gap(pool)                                                              # D reads Gb_{s-1}
@@ -240,13 +293,15 @@ def block(ST, P, HH=True, FF=True):
         for dp in dpps:
             gap(pool)
             emit(It("", f"v_max_i32_dpp %[{g}], %[{g}], %[{g}] {dp} bank_mask:0xf"))
+        carried = [it for it in pool if it.carry and not (pipe and s == PIPE_DEADLINE)]
+        pool = [it for it in pool if it not in carried]
         while pool:
             got = take(pool, 1, ())
             assert got, [p.name for p in pool]
             emit(got[0])
     # tail: D and F of column 7, its codes / scores / ring write, then prog
     done.discard("F")
-    pool = column_items(7, ST, HH, FF)
+    pool = (ring_items(7) + carried) if pipe else column_items(7, ST, HH, FF)
     if READ_AT >= 8:
         pool = reads + pool
     gap(pool)
@@ -256,11 +311,13 @@ def block(ST, P, HH=True, FF=True):
         got = take(pool, 1, ())
         assert got, [p.name for p in pool]
         emit(got[0])
-    if FF:
+    if FF and not pipe:
         emit(It("", "v_xor_b32_e32 %[accA], 0xffffff, %[accA]"))            # flags were collected inverted
         emit(It("", "v_xor_b32_e32 %[accB], 0xffffff, %[accB]"))
     emit(It("PW", "ds_write_b32 %[cb], %[cv] offset:16", lds=True))         # prog[w+1] = c+1
     lines = [it.text for it in out]
+    if pipe:
+        lines = [re.sub(r"%\[(\w+)\]", lambda m: PIPE_REGS.get(m.group(1), m.group(0)), ln) for ln in lines]
     if ALIGN is not None:
         # start the block at a fixed place in a 64-byte line (MI355X_MICROARCH.md,
         # "Code-placement sensitivity"), jumping over the padding: the block's
@@ -277,7 +334,7 @@ def check(lines):
     """DPP sources: two wait states (instructions, or s_nop N = N + 1) after the
     VALU that wrote them."""
     def dst(x):
-        if x.startswith(("ds_", "s_")):
+        if x.startswith(("ds_", "s_", "global_")):
             return None
         return x.split()[1].rstrip(",")
 
@@ -392,6 +449,31 @@ def main():
                 f"(PairRegs& r, const PairConst& k, PairSlot& ts, PairSlot& ns, int cv, int ra, int rd) {{\n"
                 f"{decl}    asm volatile(\n{cstr(lines)}\n{ops}"
                 f"        : \"vcc\", \"memory\");\n}}\n")
+    # The pipelined raw block (scores + codes): see the module docstring.
+    parts.append("template <bool P>\n"
+                 "__device__ __forceinline__ void pair_chunk_pipe(PairRegs& r, const PairConst& k, PairSlot& ts,\n"
+                 "                                                PairSlot& ns, int cv, int ra, int rd, int voa, int vob,\n"
+                 "                                                int vda, int vdb, const int32_t* hbs, const int32_t* hbp,\n"
+                 "                                                const uint32_t* dbp);\n")
+    for P in (0, 1):
+        lines = block(0, P, False, True, pipe=True)
+        nvalu = sum(1 for x in lines if x.startswith("v_"))
+        ops = operands(chr(10).join(lines))
+        ops = ops.replace("(dga_[1])", "(r.dga1)").replace("(dgb_[1])", "(r.dgb1)")
+        outs, ins = ops.rstrip("\n").split("\n")
+        outs += (', [pLa] "=&v"(p_[0]), [pUa] "=&v"(p_[1]), [pDa] "=&v"(p_[2]), [pLb] "=&v"(p_[3]), '
+                 '[pUb] "=&v"(p_[4]), [pDb] "=&v"(p_[5]), [tA] "=&v"(p_[6]), [tB] "=&v"(p_[7]), '
+                 '[qa1] "+{v[84:87]}"(r.qa1), [qb1] "+{v[92:95]}"(r.qb1)')
+        ins += (', [pdga] "v"(r.dga1), [pdgb] "v"(r.dgb1), [pA] "v"(r.accA), [pB] "v"(r.accB), [voa] "v"(voa), '
+                '[vob] "v"(vob), [vda] "v"(vda), [vdb] "v"(vdb), [hbs] "s"(hbs), [hbp] "s"(hbp), [dbp] "s"(dbp)')
+        clob = ", ".join(f'"v{n}"' for n in list(range(80, 84)) + list(range(88, 92)))
+        parts.append(f"// VALU pair_chunk_pipe<{tf(P)}>: {nvalu} per 8 columns x 128 rows\n")
+        parts.append(
+            f"template <> __device__ __forceinline__ void pair_chunk_pipe<{tf(P)}>"
+            f"(PairRegs& r, const PairConst& k, PairSlot& ts, PairSlot& ns, int cv, int ra, int rd, int voa, int vob,\n"
+            f"        int vda, int vdb, const int32_t* hbs, const int32_t* hbp, const uint32_t* dbp) {{\n"
+            f"{decl}    [[maybe_unused]] int p_[8];\n    asm volatile(\n{cstr(lines)}\n{outs}\n{ins}\n"
+            f"        : \"vcc\", \"memory\", {clob});\n}}\n")
     with open(args.out, "w") as f:
         f.write("\n".join(parts))
     print("wrote", args.out)

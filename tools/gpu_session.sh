@@ -23,7 +23,8 @@ for step in "$@"; do
     bench)    run 600 bench python bench.py > $OUT/${TAG}_bench.json 2> $OUT/${TAG}_bench.err || { cat $OUT/${TAG}_bench.err; exit 1; }
               cat $OUT/${TAG}_bench.json ;;
     ab:*)     ARGS=${step#ab:}
-              run 1100 "ab $ARGS" python3 tools/ab_run.py --libs 'lib_ab/*.so' $ARGS 2>&1 | tee -a $OUT/${TAG}_ab.txt || exit 1 ;;
+              LIBS=(); compgen -G 'lib_ab/*.so' > /dev/null && LIBS=(--libs 'lib_ab/*.so')   # (none built: the in-tree library)
+              run 1100 "ab $ARGS" python3 tools/ab_run.py "${LIBS[@]}" $ARGS 2>&1 | tee -a $OUT/${TAG}_ab.txt || exit 1 ;;
     run:*)    CMD=${step#run:}
               run 1100 "$CMD" bash -c "$CMD" 2>&1 | tee -a $OUT/${TAG}_run.txt || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
