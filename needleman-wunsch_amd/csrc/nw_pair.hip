@@ -82,8 +82,8 @@ struct PairRegs {
     // pair_chunk_pipe (raw scores + codes, pipelined across blocks): G' of
     // columns 4..7 of rows a / b in fixed registers (.w = the carried ga / gb),
     // column 7's diagonal candidates, and accA / accB = the block's code words
-    // still without column 7 (flags inverted); the next block -- or
-    // flush_pending -- finishes and stores them.
+    // still without column 7; the next block -- or flush_pending -- finishes
+    // and stores them.
     v4i qa1, qb1;
     int dga1, dgb1;
 };
@@ -420,12 +420,10 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
             asm volatile("" : "+v"(voa), "+v"(vob), "+v"(vda), "+v"(vdb));
             auto flush_pending = [&]() {
                 if (PIPE && pend >= 0) {
-                    auto lt = [](int x, int y) { return ((uint32_t)x - (uint32_t)y) >> 31; };   // 1: x < y (a flag not set)
+                    auto eq = [](int x, int y) { return x == y ? 1u : 0u; };   // a candidate that attains the max
                     const int ga6 = r.qa1[2], ga7 = r.qa1[3], gb6 = r.qb1[2], gb7 = r.qb1[3];
-                    const uint32_t accA =
-                        ((r.accA << 3) | (lt(ga6, ga7) << 2) | (lt(r.sh, ga7) << 1) | lt(r.dga1, ga7)) ^ 0xffffffu;
-                    const uint32_t accB =
-                        ((r.accB << 3) | (lt(gb6, gb7) << 2) | (lt(ga7, gb7) << 1) | lt(r.dgb1, gb7)) ^ 0xffffffu;
+                    const uint32_t accA = (r.accA << 3) | (eq(ga6, ga7) << 2) | (eq(r.sh, ga7) << 1) | eq(r.dga1, ga7);
+                    const uint32_t accB = (r.accB << 3) | (eq(gb6, gb7) << 2) | (eq(ga7, gb7) << 1) | eq(r.dgb1, gb7);
                     __builtin_nontemporal_store(r.qa1, reinterpret_cast<v4i*>(tileA + (int64_t)pend * 512 + 256 + lane * 4));
                     __builtin_nontemporal_store(r.qb1, reinterpret_cast<v4i*>(tileB + (int64_t)pend * 512 + 256 + lane * 4));
                     __builtin_nontemporal_store(accA, dtileA + (int64_t)(pend + 1) * 64 + lane);

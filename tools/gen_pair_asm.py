@@ -18,9 +18,10 @@ Lane l holds rows a = 2l and b = 2l + 1 of a 128-row stripe.  Column step s
 Step 0 takes sh_0, Ga_{-1}, Gb_{-1} from the previous block (its tail runs D
 and F for column 7).  Every DPP needs two instructions after the VALU that
 wrote its source; those gaps take the previous column's work: its two code
-words (candidate - G' is 0 exactly for the candidates that attain the max,
-so the sign bit of one v_sub is the inverted flag, shifted in with
-v_alignbit_b32), its scores H = G' + nlo + kd, the ring write of lane 63's
+words (a flag is v_cmp_eq_u32_e32 candidate, G' into VCC and
+v_addc_co_u32_e32 acc = 2 acc + VCC -- two 4-byte encodings: a lone wave's
+time follows the bytes of code it fetches, and a subtract plus v_alignbit_b32
+is 12), its scores H = G' + nlo + kd, the ring write of lane 63's
 Gb (the row above of the wave below), the lane-0 pre-fill of the next shift
 and the chunk's LDS traffic (cons, the next slot's {prog, cons}, 8 T and the
 chunk's symbols, the symbols down the ring, prog after the last ring write).
@@ -105,8 +106,18 @@ def T(s):
 
 
 class It:
+    """One schedulable item: one instruction, or two that must stay together
+    (a compare into VCC and the add-with-carry that consumes it)."""
     def __init__(self, name, text, deps=(), lds=False, carry=False):
         self.name, self.text, self.deps, self.lds, self.carry = name, text, list(deps), lds, carry
+        self.n = text.count("\n") + 1
+
+
+def flag(name, acc, cand, g, deps=(), src=None, **kw):
+    """acc = 2 * src + (cand == g): one direction flag shifted into a code word."""
+    src = src or acc
+    return It(name, f"v_cmp_eq_u32_e32 vcc, %[{cand}], %[{g}]\n"
+                    f"v_addc_co_u32_e32 %[{acc}], vcc, %[{src}], %[{src}], vcc", deps, **kw)
 
 
 def deferred_items():
@@ -114,25 +125,16 @@ def deferred_items():
     columns 6, 7 are still in the fixed registers, its dg and shift in carried
     operands), code words and stores of columns 4..7."""
     C = dict(carry=True)
-    its = [It("pLb", "v_sub_u32_e32 %[pLb], %[gb6], %[gbc]", **C),
-           It("pDb", "v_sub_u32_e32 %[pDb], %[pdgb], %[gbc]", **C),
-           It("pUb", "v_sub_u32_e32 %[pUb], %[gac], %[gbc]", **C),
-           It("pLa", "v_sub_u32_e32 %[pLa], %[ga6], %[gac]", **C),
-           It("pUa", "v_sub_u32_e32 %[pUa], %[shc], %[gac]", **C),
-           It("pDa", "v_sub_u32_e32 %[pDa], %[pdga], %[gac]", **C),
-           It("sQb1", "global_store_dwordx4 %[vob], v[92:95], %[hbp] offset:1024 nt", **C),
-           It("sQa1", "global_store_dwordx4 %[voa], v[84:87], %[hbp] offset:1024 nt", **C),
-           It("qA1", "v_alignbit_b32 %[tA], %[pA], %[pLa], 31", ["pLa"], **C),
-           It("qB1", "v_alignbit_b32 %[tB], %[pB], %[pLb], 31", ["pLb"], **C),
-           It("qA2", "v_alignbit_b32 %[tA], %[tA], %[pUa], 31", ["pUa", "qA1"], **C),
-           It("qB2", "v_alignbit_b32 %[tB], %[tB], %[pUb], 31", ["pUb", "qB1"], **C),
-           It("qA3", "v_alignbit_b32 %[tA], %[tA], %[pDa], 31", ["pDa", "qA2"], **C),
-           It("qB3", "v_alignbit_b32 %[tB], %[tB], %[pDb], 31", ["pDb", "qB2"], **C),
-           It("xA", "v_xor_b32_e32 %[tA], 0xffffff, %[tA]", ["qA3"], **C),
-           It("xB", "v_xor_b32_e32 %[tB], 0xffffff, %[tB]", ["qB3"], **C),
-           It("stA", "global_store_dword %[vda], %[tA], %[dbp] nt", ["xA"], **C),
-           It("stB", "global_store_dword %[vdb], %[tB], %[dbp] nt", ["xB"], **C)]
-    return its
+    return [flag("qB1", "tB", "gb6", "gbc", src="pB", **C),
+            flag("qA1", "tA", "ga6", "gac", src="pA", **C),
+            It("sQb1", "global_store_dwordx4 %[vob], v[92:95], %[hbp] offset:1024 nt", **C),
+            It("sQa1", "global_store_dwordx4 %[voa], v[84:87], %[hbp] offset:1024 nt", **C),
+            flag("qB2", "tB", "gac", "gbc", ["qB1"], **C),
+            flag("qA2", "tA", "shc", "gac", ["qA1"], **C),
+            flag("qB3", "tB", "pdgb", "gbc", ["qB2"], **C),
+            flag("qA3", "tA", "pdga", "gac", ["qA2"], **C),
+            It("stA", "global_store_dword %[vda], %[tA], %[dbp] nt", ["qA3"], **C),
+            It("stB", "global_store_dword %[vdb], %[tB], %[dbp] nt", ["qB3"], **C)]
 
 
 def sub_items(s, P, row):
@@ -171,28 +173,22 @@ def column_items(c, ST, HH=True, FF=True):
         return its + [It("Hb", f"v_add3_u32 %[hb{c}], %[{GB(c)}], %[nlob], %[kd{c}]"),
                       It("Ha", f"v_add3_u32 %[ha{c}], %[{GA(c)}], %[nloa], %[kd{c}]", ["F"])]
     its = []
-    # row b parts need no F
-    its.append(It("Lb", f"v_sub_u32_e32 %[dLb], %[{GB(c - 1)}], %[{GB(c)}]"))
+    n = lambda x: f"{x}{c}"      # (a dependency must not be met by an earlier column's item)
+    # row b's left flag needs no F (row a's final max); the code of a column
+    # is left, up, diag from the top: shifted in in that order
+    its.append(flag(n("Lb"), "accB", GB(c - 1), GB(c)))
     if HH:
         its.append(It("Hb", f"v_add3_u32 %[hb{c}], %[{GB(c)}], %[nlob], %[kd{c}]"))
     its += ring_items(c)
-    its.append(It("Db", f"v_sub_u32_e32 %[dDb], %[{DGB(c)}], %[{GB(c)}]"))
-    its.append(It("Ub", f"v_sub_u32_e32 %[dUb], %[{GA(c)}], %[{GB(c)}]", ["F"]))
-    its.append(It("La", f"v_sub_u32_e32 %[dLa], %[{GA(c - 1)}], %[{GA(c)}]", ["F"]))
-    its.append(It("Ua", f"v_sub_u32_e32 %[dUa], %[{SH(c + 1)}], %[{GA(c)}]", ["F"]))
-    its.append(It("Da", f"v_sub_u32_e32 %[dDa], %[{DGA(c)}], %[{GA(c)}]", ["F"]))
+    its.append(flag(n("La"), "accA", GA(c - 1), GA(c), ["F"]))
+    its.append(flag(n("Ub"), "accB", GA(c), GB(c), ["F", n("Lb")]))
+    its.append(flag(n("Ua"), "accA", SH(c + 1), GA(c), ["F", n("La")]))
+    its.append(flag(n("Db"), "accB", DGB(c), GB(c), [n("Ub")]))
+    its.append(flag(n("Da"), "accA", DGA(c), GA(c), ["F", n("Ua")]))
     if HH:
         its.append(It("Ha", f"v_add3_u32 %[ha{c}], %[{GA(c)}], %[nloa], %[kd{c}]", ["F"]))
-    hiA = "0" if c == 0 else "%[accA]"
-    hiB = "0" if c == 0 else "%[accB]"
-    its.append(It("bA1", f"v_alignbit_b32 %[accA], {hiA}, %[dLa], 31", ["La"]))
-    its.append(It("bB1", f"v_alignbit_b32 %[accB], {hiB}, %[dLb], 31", ["Lb"]))
-    its.append(It("bA2", "v_alignbit_b32 %[accA], %[accA], %[dUa], 31", ["Ua", "bA1"]))
-    its.append(It("bB2", "v_alignbit_b32 %[accB], %[accB], %[dUb], 31", ["Ub", "bB1"]))
-    its.append(It("bA3", "v_alignbit_b32 %[accA], %[accA], %[dDa], 31", ["Da", "bA2"]))
-    its.append(It("bB3", "v_alignbit_b32 %[accB], %[accB], %[dDb], 31", ["Db", "bB2"]))
     if EXP_FLAGS9:
-        its = [it for it in its if it.name not in ("bB1", "bB2", "bB3")]
+        its = [it for it in its if it.name not in (n("Lb"), n("Ub"), n("Db"))]
     if ST:
         its.append(It("Za", f"v_sub_u32_e32 %[tmp], 0, %[ha{c}]", ["Ha"]))
         its.append(It("Ma", f"v_max3_i32 %[gavA], %[gavA], %[ha{c}], %[tmp]", ["Za"]))
@@ -210,23 +206,28 @@ def block(ST, P, HH=True, FF=True, pipe=False):
         out.append(it)
         done.add(it.name)
 
-    def take(pool, k, ready):
+    def take(pool, k, ready, slots=99):
+        """Up to k ready items of the pool, in its order, of at most `slots`
+        instructions together."""
         got = []
         for it in list(pool):
-            if len(got) == k:
+            if len(got) == k or slots == 0:
                 break
-            if all(d_ in done or d_ in ready or d_ in [g.name for g in got] for d_ in it.deps):
+            if it.n <= slots and all(d_ in done or d_ in ready or d_ in [g.name for g in got] for d_ in it.deps):
                 got.append(it)
+                slots -= it.n
                 pool.remove(it)
         return got
 
     def gap(pool, ready=()):
-        got = take(pool, 2, ready)
+        """The two wait states before a DPP instruction."""
+        got = take(pool, 2, ready, slots=2)
         for g in got:
             emit(g)
-        if len(got) == 1:
+        n = sum(g.n for g in got)
+        if n == 1:
             out.append(It("", "s_nop 0"))
-        elif not got:
+        elif n == 0:
             out.append(It("", "s_nop 1"))
 
     sym = ([It("W8", "ds_write2_b32 %[ra], %[tc0], %[tc1] offset0:8 offset1:9", lds=True)] if RING2 else
@@ -254,6 +255,8 @@ def block(ST, P, HH=True, FF=True, pipe=False):
                 It("", "v_perm_b32 %[subA1], %[pha], %[pla], %[tc1]"),
                 It("", "v_perm_b32 %[subB0], %[phb], %[plb], %[tc0]"),
                 It("", "v_perm_b32 %[subB1], %[phb], %[plb], %[tc1]")]
+    if FF:
+        out += [It("", "v_mov_b32_e32 %[accA], 0"), It("", "v_mov_b32_e32 %[accB], 0")]
     for s in range(8):
         done.discard("F")
         pool = []
@@ -311,11 +314,8 @@ def block(ST, P, HH=True, FF=True, pipe=False):
         got = take(pool, 1, ())
         assert got, [p.name for p in pool]
         emit(got[0])
-    if FF and not pipe:
-        emit(It("", "v_xor_b32_e32 %[accA], 0xffffff, %[accA]"))            # flags were collected inverted
-        emit(It("", "v_xor_b32_e32 %[accB], 0xffffff, %[accB]"))
     emit(It("PW", "ds_write_b32 %[cb], %[cv] offset:16", lds=True))         # prog[w+1] = c+1
-    lines = [it.text for it in out]
+    lines = [ln for it in out for ln in it.text.split("\n")]
     if pipe:
         lines = [re.sub(r"%\[(\w+)\]", lambda m: PIPE_REGS.get(m.group(1), m.group(0)), ln) for ln in lines]
     if ALIGN is not None:
