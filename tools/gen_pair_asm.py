@@ -51,7 +51,7 @@ import re
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 OUT = os.path.join(ROOT, "needleman-wunsch_amd", "csrc", "nw_pair_chunk.inc")
-READ_AT = 6            # step whose gaps issue the next slot's progress and data reads
+READ_AT = 3            # step whose gaps issue the next slot's progress and data reads
 ALIGN = None           # None, or the byte phase (0 / 4) mod 8 at which every block starts
 # The DPP shift of column s writes into the register of T_{s-1} (the row
 # above at column s-1, not needed after column s-1's max3): lanes >= 1 take

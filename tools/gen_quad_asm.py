@@ -42,7 +42,7 @@ import re
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 OUT = os.path.join(ROOT, "needleman-wunsch_amd", "csrc", "nw_quad_chunk.inc")
-READ_AT = 5            # step whose gaps issue the next slot's progress and data reads
+READ_AT = 6            # step whose gaps issue the next slot's progress and data reads
 
 
 def G(s):
