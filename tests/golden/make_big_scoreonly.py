@@ -1,4 +1,4 @@
-"""Pin the 1M x 1M score-only fill (BASELINE configs[4]) with the CPU restatement.
+"""Pin the 1M x 1M score-only fill (BASELINE.json configs[4]) with the CPU restatement.
 
     python tests/golden/make_big_scoreonly.py [threads]
 
