@@ -535,7 +535,10 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                     __builtin_amdgcn_s_sleep(1);
                 }
             };
-            auto full_chunk = [&](int c, auto slotc, PairSlot& cur, PairSlot& nxt, bool head = false) -> bool {
+            // (head: the first chunk of a run; mid: another full chunk follows --
+            // constants at every call, so the checks they spare are compiled out)
+            auto full_chunk = [&](int c, auto slotc, PairSlot& cur, PairSlot& nxt, bool head = false,
+                                  bool mid = false) -> bool {
                 constexpr int Q = decltype(slotc)::value;
                 if constexpr (PIPE) {
                     // The block stores the pending chunk's second half and code
@@ -555,8 +558,10 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                     }
                     pair_chunk_pipe<PROF>(r, kc, cur, nxt, c + 1, ra[Q], rd[(Q + 1) % R], voa, vob, vda, vdb, hbs, hbp, dbp);
                     pend = c;
-                    if (c + 2 >= NC) return true;
-                    if (uni((int)(uint32_t)r.pq) > c + 1 && uni((int)(r.pq >> 32)) >= c + 2 - R) return true;
+                    if (!mid && c + 2 >= NC) return true;
+                    // (prog[w] > c + 1 and cons[w+1] >= c + 2 - R, as one sign test: the common case falls through)
+                    if (__builtin_expect(((uni((int)(uint32_t)r.pq) - (c + 2)) | (uni((int)(r.pq >> 32)) - (c + 2 - R))) >= 0, 1))
+                        return true;
                     return wait_slot(c + 1, nxt);
                 } else if constexpr (RAW) {
                     pair_chunk_raw<SD, PROF>(r, kc, cur, nxt, c + 1, ra[Q], rd[(Q + 1) % R]);
@@ -581,8 +586,10 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                     r.nloa -= CH * d;
                     r.nlob -= CH * d;
                 }
-                if (c + 2 >= NC) return true;          // the next chunk is the generic last one
-                if (uni((int)(uint32_t)r.pq) > c + 1 && uni((int)(r.pq >> 32)) >= c + 2 - R) return true;
+                if (!mid && c + 2 >= NC) return true;  // the next chunk is the generic last one
+                // (prog[w] > c + 1 and cons[w+1] >= c + 2 - R, as one sign test: the common case falls through)
+                if (__builtin_expect(((uni((int)(uint32_t)r.pq) - (c + 2)) | (uni((int)(r.pq >> 32)) - (c + 2 - R))) >= 0, 1))
+                    return true;
                 return wait_slot(c + 1, nxt);
             };
             using S0 = std::integral_constant<int, 0>;
@@ -592,13 +599,13 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
             int c = 0;
             const int nfull = NC - 1;                  // chunks before the last one
             if (nfull > 0) aborted = !wait_slot(0, tA);
-            while (c + R <= nfull && !aborted) {
+            while (c + R < nfull && !aborted) {
                 rebase(c);
                 // [8*NSW + g]: when this stripe reaches the middle of the table
                 if (NW_TRACE_EXT && a.trace && lane == 0 && c == trace_mid_chunk(NC, R))
                     *trace_ext(a, TX_MID, g) = __builtin_amdgcn_s_memrealtime();
-                aborted = !full_chunk(c, S0{}, tA, tB, true) || !full_chunk(c + 1, S1{}, tB, tA) ||
-                          !full_chunk(c + 2, S2{}, tA, tB) || !full_chunk(c + 3, S3{}, tB, tA);
+                aborted = !full_chunk(c, S0{}, tA, tB, true, true) || !full_chunk(c + 1, S1{}, tB, tA, false, true) ||
+                          !full_chunk(c + 2, S2{}, tA, tB, false, true) || !full_chunk(c + 3, S3{}, tB, tA, false, true);
                 c += R;
             }
             if (!aborted && c < nfull) {
@@ -606,6 +613,7 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_pair_kernel(FillArgs a) {
                 aborted = !full_chunk(c, S0{}, tA, tB, true);
                 if (!aborted && c + 1 < nfull) aborted = !full_chunk(c + 1, S1{}, tB, tA);
                 if (!aborted && c + 2 < nfull) aborted = !full_chunk(c + 2, S2{}, tA, tB);
+                if (!aborted && c + 3 < nfull) aborted = !full_chunk(c + 3, S3{}, tB, tA);
                 c = nfull;
             }
             if (!aborted) {

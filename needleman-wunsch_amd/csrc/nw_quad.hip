@@ -432,7 +432,9 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_quad_kernel(FillArgs a) {
                 if (SD) __builtin_nontemporal_store(r.acc, dtile + (int64_t)(c + 1) * 64 + lane);
                 r.ptc1 = (uint32_t)cur.c[1];
                 if (!more) return true;                // the next block is a generic one
-                if (uni((int)(uint32_t)r.pq) > c + 1 && uni((int)(r.pq >> 32)) >= c + 2 - R) return true;
+                // (prog[w] > c + 1 and cons[w+1] >= c + 2 - R, as one sign test: the common case falls through)
+                if (__builtin_expect(((uni((int)(uint32_t)r.pq) - (c + 2)) | (uni((int)(r.pq >> 32)) - (c + 2 - R))) >= 0, 1))
+                    return true;
                 return wait_slot(c + 1, nxt);
             };
             using S0 = std::integral_constant<int, 0>;
@@ -447,6 +449,9 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_quad_kernel(FillArgs a) {
             if (!aborted && c < cend) {
                 aborted = !wait_slot(c, tB);           // block 1 sits in ring slot 1
                 // blocks are unrolled by ring slot: c % 4 = 1, 2, 3, 0
+                // (one loop with an end check per block: the same blocks in groups
+                // of four without end checks ran 1.6% slower -- code placement,
+                // profiles/r04n_ab_interblock.txt)
                 while (!aborted && c < cend) {
                     const bool m1 = c + 1 < cend, m2 = c + 2 < cend, m3 = c + 3 < cend, m4 = c + 4 < cend;
                     aborted = !full_block(c, S1{}, tB, tA, m1);
