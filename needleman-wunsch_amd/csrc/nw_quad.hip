@@ -86,7 +86,8 @@ struct QuadRegs {
     int h[8];           // out: G' of the block's 8 steps (raw scores)
     uint32_t acc;       // out: the block's code word
     uint64_t pq;        // out: {prog[w], cons[w+1]} read mid-block
-    uint32_t ptc1;      // in: symbols 4..7 of the previous chunk
+    uint32_t ptc1;      // in/out: symbols 4..7 of the previous / this chunk
+    int cv;             // in/out: the block's chunk + 1 (cons[w] when its slot is taken; prog[w+1] = cv - 1)
 };
 struct QuadConst {
     uint32_t c2;        // side symbol of this lane's row
@@ -346,6 +347,7 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_quad_kernel(FillArgs a) {
             r.g = r.sh = C0;
             r.pq = 0;
             r.ptc1 = 0;
+            r.cv = 0;
             bool aborted = false;
             if (a.trace && lane == 0 && w == 0) {
                 a.trace[8 * (int64_t)sidx + 1] = __builtin_amdgcn_s_memrealtime();
@@ -426,11 +428,10 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_quad_kernel(FillArgs a) {
             };
             auto full_block = [&](int c, auto slotc, QuadSlot& cur, QuadSlot& nxt, bool more) -> bool {
                 constexpr int Q = decltype(slotc)::value;
-                quad_chunk_asm<SH, SD, PROF>(r, kc, cur, nxt, c, ra[Q], ra[(Q + R - 1) % R], rd[(Q + 1) % R]);
+                quad_chunk_asm<SH, SD, PROF>(r, kc, cur, nxt, ra[Q], ra[(Q + R - 1) % R], rd[(Q + 1) % R]);
                 r.h[7] = r.g;
                 if (SH) quad_store_scores(r.h, tile + (int64_t)c * 512 + lane * 4);
                 if (SD) __builtin_nontemporal_store(r.acc, dtile + (int64_t)(c + 1) * 64 + lane);
-                r.ptc1 = (uint32_t)cur.c[1];
                 if (!more) return true;                // the next block is a generic one
                 // (prog[w] > c + 1 and cons[w+1] >= c + 2 - R, as one sign test: the common case falls through)
                 if (__builtin_expect(((uni((int)(uint32_t)r.pq) - (c + 2)) | (uni((int)(r.pq >> 32)) - (c + 2 - R))) >= 0, 1))
@@ -448,6 +449,7 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_quad_kernel(FillArgs a) {
 #if NW_QUAD_ASM
             if (!aborted && c < cend) {
                 aborted = !wait_slot(c, tB);           // block 1 sits in ring slot 1
+                r.cv = c + 1;
                 // blocks are unrolled by ring slot: c % 4 = 1, 2, 3, 0
                 // (one loop with an end check per block: the same blocks in groups
                 // of four without end checks ran 1.6% slower -- code placement,

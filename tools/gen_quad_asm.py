@@ -90,7 +90,9 @@ def column_items(c, FF):
     """Code (FF) and ring write of step c (the up flag needs sh_{c+1}: dep 'D')."""
     its = [ring_item(c)]
     if c == 2:      # the previous chunk's slot is complete: the wave below may take it
-        its.append(It("PW", "ds_write_b32 %[cb], %[cvp] offset:16", ["R2"], lds=True))
+        its.append(It("PV", "v_add_u32_e32 %[cvp], -1, %[cv]"))             # prog[w+1] = c: chunk c - 1 complete
+        its.append(It("PW", "ds_write_b32 %[cb], %[cvp] offset:16", ["R2", "PV"], lds=True))
+        its.append(It("CV", "v_add_u32_e32 %[cv], 1, %[cv]", ["PV", "CW"]))    # the next block's chunk
     if not FF:
         return its
     its.append(It(f"L{c}", f"v_sub_u32_e32 %[dL], %[{G(c - 1)}], %[{G(c)}]"))
@@ -148,6 +150,10 @@ def block(P, FF):
         if s > 0:
             pool += column_items(s - 1, FF)
         pool += mem.get(s, [])
+        if s == 1:
+            # the next block's window starts in this chunk's symbols 4..7: carried in
+            # place (a copy between the blocks costs an instruction and a branch there)
+            pool.append(It("PT", "v_mov_b32_e32 %[ptc1], %[tc1]"))
         if s > 0:
             gap(pool)                                                              # C, D read G_{s-1}
         emit(It("C", f"v_mov_b32_dpp %[{T(s)}], %[{G(s - 1)}] row_bcast:15 row_mask:0xe bank_mask:0xf"))
@@ -215,12 +221,12 @@ OPERANDS = r'''
       [g4] "=&v"(r.h[4]), [g5] "=&v"(r.h[5]), [g6] "=&v"(r.h[6]), [gc] "+v"(r.g), [shc] "+v"(r.sh),
       [dg0] "=&v"(dg_[0]), [dg1] "=&v"(dg_[1]), [dL] "=&v"(t_[0]), [dU] "=&v"(t_[1]), [dD] "=&v"(t_[2]),
       [sub] "=&v"(t_[3]), [tq0] "=&v"(tq_[0]), [tq1] "=&v"(tq_[1]), [sub0] "=&v"(sp_[0]), [sub1] "=&v"(sp_[1]),
-      [acc] "=&v"(r.acc), [pq] "=&v"(r.pq), [nA] "=&v"(ns.a), [nB] "=&v"(ns.b), [nC] "=&v"(ns.c),
+      [acc] "=&v"(r.acc), [ptc1] "+v"(r.ptc1), [cv] "+v"(r.cv), [cvp] "=&v"(t_[4]), [pq] "=&v"(r.pq), [nA] "=&v"(ns.a), [nB] "=&v"(ns.b), [nC] "=&v"(ns.c),
       [ta0] "+v"(ts.a[0]), [ta1] "+v"(ts.a[1]), [ta2] "+v"(ts.a[2]), [ta3] "+v"(ts.a[3]),
       [tb0] "+v"(ts.b[0]), [tb1] "+v"(ts.b[1]), [tb2] "+v"(ts.b[2]), [tb3] "+v"(ts.b[3])
-    : [tc0] "v"(ts.c[0]), [tc1] "v"(ts.c[1]), [ptc1] "v"(r.ptc1), [selq] "v"(k.selq),
+    : [tc0] "v"(ts.c[0]), [tc1] "v"(ts.c[1]), [selq] "v"(k.selq),
       [c2] "v"(k.c2), [vcm] "v"(k.vcm), [vck] "v"(k.vck), [pl] "v"(k.pl), [ph] "v"(k.ph),
-      [cb] "v"(k.cb), [cv] "v"(cv), [cvp] "v"(cvp), [ra] "v"(ra), [rap] "v"(rap), [rd] "v"(rd)
+      [cb] "v"(k.cb), [ra] "v"(ra), [rap] "v"(rap), [rd] "v"(rd)
 '''
 
 
@@ -245,12 +251,12 @@ def main():
     args = ap.parse_args()
     globals()["READ_AT"] = args.read_at
     parts = ["// GENERATED by tools/gen_quad_asm.py -- do not edit; see the generator for the schedule.\n",
-             "// c: the block's chunk; ra / rap: ring slot addresses of chunk c and c - 1; rd: the next slot.\n"
+             "// r.cv: the block's chunk + 1 (counted on in the block); ra / rap: ring slot addresses of\n"
+             "// that chunk and the one before; rd: the next slot.\n"
              "template <bool HH, bool FF, bool P>\n"
              "__device__ __forceinline__ void quad_chunk_asm(QuadRegs& r, const QuadConst& k, QuadSlot& ts,\n"
-             "                                               QuadSlot& ns, int c, int ra, int rap, int rd);\n"]
-    decl = ("    [[maybe_unused]] int dg_[2], t_[4];\n    [[maybe_unused]] uint32_t tq_[2], sp_[2];\n"
-            "    const int cv = c + 1, cvp = c;   // cons[w] = c + 1 (slot taken); prog[w+1] = c (chunk c - 1 complete)\n")
+             "                                               QuadSlot& ns, int ra, int rap, int rd);\n"]
+    decl = "    [[maybe_unused]] int dg_[2], t_[5];\n    [[maybe_unused]] uint32_t tq_[2], sp_[2];\n"
     tf = lambda b: "true" if b else "false"
     for HH in (1, 0):
         for FF in (1, 0):
@@ -260,7 +266,7 @@ def main():
                 parts.append(f"// VALU quad_chunk_asm<{tf(HH)}, {tf(FF)}, {tf(P)}>: {nvalu} per 8 steps x 64 rows\n")
                 parts.append(
                     f"template <> __device__ __forceinline__ void quad_chunk_asm<{tf(HH)}, {tf(FF)}, {tf(P)}>"
-                    f"(QuadRegs& r, const QuadConst& k, QuadSlot& ts, QuadSlot& ns, int c, int ra, int rap, int rd) {{\n"
+                    f"(QuadRegs& r, const QuadConst& k, QuadSlot& ts, QuadSlot& ns, int ra, int rap, int rd) {{\n"
                     f"{decl}    asm volatile(\n{cstr(lines)}\n{operands(chr(10).join(lines))}"
                     f"        : \"vcc\", \"memory\");\n}}\n")
     with open(args.out, "w") as f:
