@@ -68,6 +68,7 @@ RING2 = True
 # the chain against the issue count on the GPU (GEN=... PAIR_ONLY=1 tools/ab_build.sh).
 EXP_NO_BCAST = False
 EXP_NO_SCORES = False
+STORE_POLICY = "nt"    # cache policy of the pipelined block's table stores
 EXP_FLAGS9 = False     # 9 flag instructions per column instead of 12 (drops row b's three shift-ins)
 # pair_chunk_pipe: the fixed VGPRs of G' (row a columns 0..7, row b columns 0..7)
 PIPE_REGS = {**{f"ga{s}": f"v{80 + s}" for s in range(7)}, "gac": "v87",
@@ -316,6 +317,9 @@ def block(ST, P, HH=True, FF=True, pipe=False):
         emit(got[0])
     emit(It("PW", "ds_write_b32 %[cb], %[cv] offset:16", lds=True))         # prog[w+1] = c+1
     lines = [ln for it in out for ln in it.text.split("\n")]
+    if pipe and STORE_POLICY != "nt":
+        lines = [re.sub(r" nt$", (" " + STORE_POLICY).rstrip(), ln) if ln.startswith("global_store") else ln
+                 for ln in lines]
     if pipe:
         lines = [re.sub(r"%\[(\w+)\]", lambda m: PIPE_REGS.get(m.group(1), m.group(0)), ln) for ln in lines]
     if ALIGN is not None:
@@ -407,10 +411,13 @@ def main():
     ap.add_argument("--exp-no-bcast", action="store_true")
     ap.add_argument("--exp-no-scores", action="store_true")
     ap.add_argument("--exp-flags9", action="store_true")
+    ap.add_argument("--store-policy", default="nt", help="cache policy suffix of the pipelined block's table stores "
+                    "(nt | sc1 | sc0+sc1 | none); anything but nt is a timing experiment")
     args = ap.parse_args()
     globals()["EXP_NO_BCAST"] = args.exp_no_bcast
     globals()["EXP_NO_SCORES"] = args.exp_no_scores
     globals()["EXP_FLAGS9"] = args.exp_flags9
+    globals()["STORE_POLICY"] = "" if args.store_policy == "none" else args.store_policy.replace("+", " ")
     globals()["READ_AT"] = args.read_at
     globals()["ALIGN"] = args.align
     parts = ["// GENERATED by tools/gen_pair_asm.py -- do not edit; see the generator for the schedule.\n",
