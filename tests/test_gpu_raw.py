@@ -6,7 +6,7 @@ domain (G' = H + r*d + (i - base)*d, the "raw" tiles of nw_pair.hip) and uses
 a separately generated 8-column block; every reader subtracts the affine
 offset, which depends on the fill's WG-stripe plan and on the cell's
 4096-column super-chunk.  Every fill test elsewhere asks for stats too and so
-never takes that path; these tests do, on all three kernels, cell by cell
+never takes that path; these tests do, on all four kernels, cell by cell
 against the CPU oracle (needleman-wunsch.c:418-510 scores, :485-503 flags),
 and at 100k x 100k against the whole-table hashes of
 tests/golden/big_colchain.json.
