@@ -948,7 +948,11 @@ int fill_launch(nw_table* t, int32_t m, int32_t k, int32_t d, uint32_t out_mask)
             // equal, profiles/r03m_ab_quad.txt)
             const int64_t simds = 4 * (int64_t)t->ncu;
             pair = t->NG > simds;
-            skew = !pair && t->NG <= simds && L1 >= 32 * L2;
+            // (against the quad kernel the skew kernel only wins on a single
+            // stripe: 100k x 64 4.54 vs 5.15 ms, but 100k x 256 5.73 vs 5.16,
+            // 1M x 20k 61.1 vs 53.2 ms, profiles/r05l_ab_skew_vs_quad.txt; fills
+            // with stats choose between skew and scan as before)
+            skew = !pair && t->NG <= simds && L1 >= 32 * L2 && (stt || t->NG == 1);
             autosel = true;
         }
         // a feeding panel's last row must be lane 63's row b of its last pair stripe
