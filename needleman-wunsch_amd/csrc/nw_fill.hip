@@ -547,7 +547,9 @@ __global__ __launch_bounds__(64 * (W + 2)) void nw_fill_kernel(FillArgs a) {
 #endif
                 after_chunk(c, Q, CH, false);
                 // (wave-uniform: every lane read the same counters)
-                if (uni((int)(uint32_t)r.pq) > c + 1 && uni((int)(r.pq >> 32)) >= c + 2 - R) return true;
+                // (prog[w] > c + 1 and cons[w+1] >= c + 2 - R, as one sign test: the common case falls through)
+                if (__builtin_expect(((uni((int)(uint32_t)r.pq) - (c + 2)) | (uni((int)(r.pq >> 32)) - (c + 2 - R))) >= 0, 1))
+                    return true;
                 return wait_slot(c + 1, rd[NQ], nxt);
             };
             using S0 = std::integral_constant<int, 0>;

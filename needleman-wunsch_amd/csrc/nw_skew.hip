@@ -432,7 +432,9 @@ __global__ __launch_bounds__(64 * (W + 1)) void nw_skew_kernel(FillArgs a) {
                 if (ST) bc += branch_codes(out_lane ? r.acc : 0u);
                 if (publish || xpublish) publish_slot(c - 8);
                 if (c + 1 >= cmid) return true;      // the next chunk is generic: it waits itself
-                if (uni((int)(uint32_t)r.pq) > c + 9 && uni((int)(r.pq >> 32)) >= c - 5 - R) return true;
+                // (prog[w] > c + 9 and cons[w+1] >= c - 5 - R, as one sign test: the common case falls through)
+                if (__builtin_expect(((uni((int)(uint32_t)r.pq) - (c + 10)) | (uni((int)(r.pq >> 32)) - (c - 5 - R))) >= 0, 1))
+                    return true;
                 return wait_slot(c + 1, nxt);
             };
             using S0 = std::integral_constant<int, 0>;
